@@ -1,0 +1,169 @@
+/*
+ * ldt.h — C-ABI of libldt.so, the MI355X (gfx950) batch-decode path that
+ * replaces lance-distributed-training's per-row PIL/torchvision transform.
+ *
+ * Drop-in boundary (reference = /root/reference, pure Python):
+ *   - to_tensor_fn  decode_tensor_image(batch, **kwargs)   lance_iterable.py:38-50
+ *       (registered at LanceDataset(..., to_tensor_fn=...) lance_iterable.py:53-59)
+ *   - collate_fn    collate_fn(batch_of_dicts)             lance_map_style.py:21-44
+ *       (registered at get_safe_loader(..., collate_fn=...) lance_map_style.py:60-69)
+ *   - samplers      ShardedBatchSampler / ShardedFragmentSampler(pad=True)
+ *                                                          lance_iterable.py:61-69
+ * The reference has no FFI of its own (it is Python over pylance/Pillow); the
+ * Python host package ldt_amd binds these symbols with ctypes, exactly as a
+ * maintainer would (INTEGRATION.md shows the stub). No torch types cross this
+ * boundary: plain pointers, sizes and an opaque hipStream_t passed as void*.
+ *
+ * Conventions
+ *   - Every function returns an int status (LDT_OK == 0, negative = error);
+ *     no C++ exception crosses the ABI. ldt_last_error() gives a message.
+ *   - Host input pointers are borrowed for the duration of the call only: the
+ *     call copies what it needs into the context's pinned staging ring before
+ *     returning. Output device pointers are owned by the caller (torch).
+ *   - Work is enqueued on `stream` (torch's current stream); results are
+ *     stream-ordered. One context per (process, device); a context is not
+ *     thread-safe.
+ */
+#ifndef LDT_H
+#define LDT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (return values) ---- */
+#define LDT_OK 0
+#define LDT_ERR_ARG -1        /* bad argument                                  */
+#define LDT_ERR_HIP -2        /* a HIP runtime call failed                     */
+#define LDT_ERR_NOMEM -3      /* host/device allocation failed                 */
+#define LDT_ERR_IMAGE -4      /* >= 1 image failed: see per_image_status       */
+
+/* ---- per-image status codes (per_image_status[i]) ---- */
+#define LDT_IMG_OK 0
+#define LDT_IMG_NOT_JPEG 1    /* no SOI / malformed marker segments            */
+#define LDT_IMG_UNSUPPORTED 2 /* progressive, arithmetic, 12-bit, CMYK, multi-scan */
+#define LDT_IMG_CORRUPT 3     /* entropy data truncated or restart markers wrong */
+#define LDT_IMG_TOO_LARGE 4   /* dimension beyond LDT_MAX_DIM                  */
+#define LDT_IMG_NULL 5        /* null cell                                     */
+
+#define LDT_MAX_DIM 8192      /* max width/height of a decoded image           */
+
+/* ---- options (ldt_set_option) ---- */
+#define LDT_OPT_SYNC_STATUS 1 /* 1 (default): decode calls wait for the stream and
+                                 report device-side per-image errors before
+                                 returning; 0: asynchronous, errors are read
+                                 later with ldt_fetch_status()                  */
+#define LDT_OPT_HUFF_MODE 2   /* 0 auto (default), 1 serial per segment,
+                                 2 parallel self-synchronising subsequences     */
+#define LDT_OPT_SUBSEQ_BITS 3 /* subsequence length for mode 2 (bits)          */
+#define LDT_OPT_PROFILE 4     /* 1: record HIP events around every stage on the
+                                 caller's stream (read with ldt_stage_times)    */
+
+/* ---- stages reported by ldt_stage_times ---- */
+#define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */
+#define LDT_STAGE_DESTUFF 1   /* coefficient clear + k_destuff                 */
+#define LDT_STAGE_HUFFMAN 2   /* k_huff_*                                      */
+#define LDT_STAGE_IDCT 3      /* k_idct                                        */
+#define LDT_STAGE_RESIZE 4    /* k_resize (fused upsample/colour/resize/store) */
+#define LDT_NUM_STAGES 5
+
+typedef struct ldt_ctx ldt_ctx;
+
+/* Normalize(mean, std) applied after ToTensor (lance_iterable.py:31). */
+typedef struct {
+  float mean[3];
+  float std[3];
+} ldt_norm;
+
+/* Create a decode context on HIP device `device`. max_batch_bytes / max_n are
+ * initial workspace hints (buffers grow on demand). Returns NULL on failure. */
+ldt_ctx *ldt_create(int device, size_t max_batch_bytes, int max_n);
+void ldt_destroy(ldt_ctx *ctx);
+const char *ldt_last_error(ldt_ctx *ctx);
+int ldt_set_option(ldt_ctx *ctx, int option, int64_t value);
+/* Library version string, e.g. "ldt 0.1.0 gfx950". */
+const char *ldt_version(void);
+
+/* decode_tensor_image / collate_fn core, Arrow `binary` column (int32 offsets).
+ *   data, offsets      : the Arrow array's data and offsets buffers (host);
+ *   arr_offset         : Array.offset (slices share buffers), in rows;
+ *   n                  : rows;
+ *   validity           : Arrow validity bitmap or NULL (a null cell -> LDT_IMG_NULL);
+ *   labels             : int64 label buffer (host) or NULL, label_offset in rows;
+ *   out_img_dev        : float32 [n, 3, 224, 224] contiguous, device;
+ *   out_lbl_dev        : int64 [n], device (ignored when labels == NULL);
+ *   norm_or_null       : NULL = ToTensor only, else Normalize(mean, std) fused;
+ *   stream             : hipStream_t (void*), 0 = null stream;
+ *   per_image_status   : int32 [n] host, written with LDT_IMG_* codes.
+ * Replaces lance_iterable.py:41-49 (to_pylist + PIL open/convert + Resize +
+ * ToTensor + stack) and lance_map_style.py:34-44. */
+int ldt_decode_batch(ldt_ctx *ctx, const uint8_t *data, const int32_t *offsets,
+                     int64_t arr_offset, int64_t n, const uint8_t *validity,
+                     const int64_t *labels, int64_t label_offset, float *out_img_dev,
+                     int64_t *out_lbl_dev, const ldt_norm *norm_or_null, void *stream,
+                     int32_t *per_image_status);
+
+/* Same, Arrow `large_binary` column (int64 offsets). */
+int ldt_decode_batch_large(ldt_ctx *ctx, const uint8_t *data, const int64_t *offsets,
+                           int64_t arr_offset, int64_t n, const uint8_t *validity,
+                           const int64_t *labels, int64_t label_offset, float *out_img_dev,
+                           int64_t *out_lbl_dev, const ldt_norm *norm_or_null, void *stream,
+                           int32_t *per_image_status);
+
+/* Device-resident input (bench / pre-staged loaders): the JPEG cells already
+ * live in HBM at data_dev (same layout as the host copy data_host, which is
+ * read only for the marker headers). offsets are int64, host, absolute byte
+ * offsets of each cell in both buffers (n+1 entries). Labels as above. */
+int ldt_decode_batch_resident(ldt_ctx *ctx, const uint8_t *data_host, const uint8_t *data_dev,
+                              const int64_t *offsets, int64_t n, const int64_t *labels,
+                              float *out_img_dev, int64_t *out_lbl_dev,
+                              const ldt_norm *norm_or_null, void *stream,
+                              int32_t *per_image_status);
+
+/* Wait for the last decode on `stream` and merge device-side per-image errors
+ * into per_image_status[n] (for LDT_OPT_SYNC_STATUS = 0). */
+int ldt_fetch_status(ldt_ctx *ctx, void *stream, int32_t *per_image_status, int64_t n);
+
+/* Profiling (LDT_OPT_PROFILE = 1): waits for every recorded stage event and
+ * adds the elapsed milliseconds of each stage since the last reset into
+ * ms_out[stage] and the number of timed launches into count_out[stage]
+ * (arrays of LDT_NUM_STAGES). reset != 0 clears the accumulators after reading. */
+int ldt_stage_times(ldt_ctx *ctx, double *ms_out, int64_t *count_out, int reset);
+
+/* Config 5: raw uint8 HWC cells (no JPEG) -> Resize(224,224) [+Normalize] ->
+ * float32 [n,3,224,224]. `hwc` is a device pointer when hwc_is_device != 0,
+ * else host (copied through the pinned ring). Cell i starts at
+ * hwc + i * cell_stride bytes and is h*w*3 bytes. */
+int ldt_resize_raw(ldt_ctx *ctx, const uint8_t *hwc, int hwc_is_device, int64_t n, int h, int w,
+                   int64_t cell_stride, float *out_img_dev, const ldt_norm *norm_or_null,
+                   void *stream);
+
+/* ShardedBatchSampler index computation (README.md:257-271), on device.
+ * Writes the rank's batch row ranges as int64 pairs [start, end) into
+ * out_ranges_dev (capacity pairs) and the pair count into *out_count_dev.
+ * Batch k = [k*B, min(k*B+B, num_rows)), rank r gets k = r, r+W, ... */
+int ldt_shard_ranges(ldt_ctx *ctx, int64_t num_rows, int64_t batch_size, int rank,
+                     int world_size, int64_t *out_ranges_dev, int64_t capacity,
+                     int64_t *out_count_dev, void *stream);
+
+/* ShardedFragmentSampler index computation (README.md:140-155), on device.
+ * fragment_rows_dev: int64 [nfrag] rows per fragment (dataset order).
+ * Writes records of 5 int64 {fragment, start, end, global_start, is_pad} for
+ * the rank's batches (fragments r, r+W, ...; batches never cross fragments)
+ * into out_dev (capacity records), and the record count into *out_count_dev.
+ * pad_to < 0: no padding. pad_to >= 0: pad the rank's list to pad_to records
+ * (the max-over-ranks count agreed by all_reduce(MAX)) with this build's rule:
+ * cycle the rank's own batches; a rank with no rows cycles the global batch
+ * list from index `rank`. *out_local_count_dev receives the unpadded count. */
+int ldt_shard_fragments(ldt_ctx *ctx, const int64_t *fragment_rows_dev, int nfrag,
+                        int64_t batch_size, int rank, int world_size, int64_t pad_to,
+                        int64_t *out_dev, int64_t capacity, int64_t *out_count_dev,
+                        int64_t *out_local_count_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDT_H */

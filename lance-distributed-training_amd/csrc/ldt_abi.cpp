@@ -1,0 +1,943 @@
+// ldt_abi.cpp — host side of libldt.so: the C-ABI declared in include/ldt.h.
+//
+// Per batch the host does planning only: it walks each cell's JPEG marker
+// segments (SOI..SOS, a few hundred bytes; the entropy-coded data is never
+// touched on the host), dedupes Huffman/quantisation tables, lays out the
+// device workspace and writes one compact plan blob (descriptors, segments,
+// tables, the ToTensor/Normalize LUT, labels, per-image status) into a pinned
+// ring slot. One H2D copy moves the plan, one moves the cells (unless they are
+// already resident), then five kernels run on the caller's stream.
+//
+// Replaces, per batch: lance_iterable.py:41-49 (to_pylist, PIL open/convert,
+// Resize, ToTensor, stack, label tensor) and lance_map_style.py:34-44.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ldt.h"
+#include "ldt_kernels.hpp"
+
+using namespace ldt;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Marker walk (ITU T.81 B.2; libjpeg jdmarker.c semantics for the subset).
+// ---------------------------------------------------------------------------
+struct RawHuff {
+  uint8_t counts[16];
+  uint8_t syms[256];
+  int nsym;
+  bool present;
+};
+
+struct Header {
+  int width = 0, height = 0, ncomp = 0;
+  int cid[4], h[4], v[4], tq[4], td[4], ta[4];
+  uint16_t q[4][64]; // natural order
+  bool qpresent[4] = {false, false, false, false};
+  RawHuff dc[4], ac[4];
+  int restart = 0;
+  bool jfif = false, adobe = false;
+  int adobe_transform = -1;
+  int64_t scan_pos = 0; // offset of entropy-coded data within the cell
+};
+
+const uint8_t kZigzagToNatural[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+inline int be16(const uint8_t *p) { return (p[0] << 8) | p[1]; }
+
+// Returns an LDT_IMG_* code.
+int walk_markers(const uint8_t *cell, int64_t len, Header &H) {
+  for (int i = 0; i < 4; ++i) H.dc[i].present = H.ac[i].present = false;
+  if (len < 4 || cell[0] != 0xFF || cell[1] != 0xD8) return LDT_IMG_NOT_JPEG;
+  int64_t i = 2;
+  bool sof = false;
+  while (true) {
+    if (i + 1 >= len) return LDT_IMG_NOT_JPEG;
+    if (cell[i] != 0xFF) return LDT_IMG_NOT_JPEG;
+    while (i + 1 < len && cell[i + 1] == 0xFF) ++i; // fill bytes
+    if (i + 1 >= len) return LDT_IMG_NOT_JPEG;
+    const int m = cell[i + 1];
+    i += 2;
+    if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+    if (m == 0xD9) return LDT_IMG_NOT_JPEG;
+    if (i + 2 > len) return LDT_IMG_NOT_JPEG;
+    const int seglen = be16(cell + i);
+    if (seglen < 2 || i + seglen > len) return LDT_IMG_NOT_JPEG;
+    const uint8_t *s = cell + i + 2;
+    const uint8_t *e = cell + i + seglen;
+    switch (m) {
+    case 0xC0:
+    case 0xC1: {
+      if (e - s < 6) return LDT_IMG_NOT_JPEG;
+      if (s[0] != 8) return LDT_IMG_UNSUPPORTED;
+      H.height = be16(s + 1);
+      H.width = be16(s + 3);
+      H.ncomp = s[5];
+      if (H.width == 0 || H.height == 0) return LDT_IMG_NOT_JPEG;
+      if (H.ncomp != 1 && H.ncomp != 3) return LDT_IMG_UNSUPPORTED;
+      if (e - s < 6 + 3 * H.ncomp) return LDT_IMG_NOT_JPEG;
+      for (int c = 0; c < H.ncomp; ++c) {
+        H.cid[c] = s[6 + 3 * c];
+        H.h[c] = s[7 + 3 * c] >> 4;
+        H.v[c] = s[7 + 3 * c] & 15;
+        H.tq[c] = s[8 + 3 * c];
+        if (H.h[c] < 1 || H.h[c] > 4 || H.v[c] < 1 || H.v[c] > 4 || H.tq[c] > 3)
+          return LDT_IMG_NOT_JPEG;
+      }
+      sof = true;
+      break;
+    }
+    case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA:
+    case 0xCB: case 0xCD: case 0xCE: case 0xCF:
+      return LDT_IMG_UNSUPPORTED;
+    case 0xC4: {
+      while (s < e) {
+        const int tc = s[0] >> 4, th = s[0] & 15;
+        if (tc > 1 || th > 3 || e - s < 17) return LDT_IMG_NOT_JPEG;
+        RawHuff &t = tc ? H.ac[th] : H.dc[th];
+        int n = 0;
+        for (int l = 0; l < 16; ++l) {
+          t.counts[l] = s[1 + l];
+          n += s[1 + l];
+        }
+        if (n > 256 || e - s < 17 + n) return LDT_IMG_NOT_JPEG;
+        memcpy(t.syms, s + 17, n);
+        t.nsym = n;
+        t.present = true;
+        s += 17 + n;
+      }
+      break;
+    }
+    case 0xDB: {
+      while (s < e) {
+        const int pq = s[0] >> 4, tq = s[0] & 15;
+        if (tq > 3 || pq > 1) return LDT_IMG_NOT_JPEG;
+        const int need = pq ? 129 : 65;
+        if (e - s < need) return LDT_IMG_NOT_JPEG;
+        for (int k = 0; k < 64; ++k)
+          H.q[tq][kZigzagToNatural[k]] = pq ? (uint16_t)be16(s + 1 + 2 * k) : s[1 + k];
+        H.qpresent[tq] = true;
+        s += need;
+      }
+      break;
+    }
+    case 0xDD:
+      if (seglen != 4) return LDT_IMG_NOT_JPEG;
+      H.restart = be16(s);
+      break;
+    case 0xE0:
+      if (e - s >= 5 && memcmp(s, "JFIF\0", 5) == 0) H.jfif = true;
+      break;
+    case 0xEE:
+      if (e - s >= 12 && memcmp(s, "Adobe", 5) == 0) {
+        H.adobe = true;
+        H.adobe_transform = s[11];
+      }
+      break;
+    case 0xDA: {
+      if (!sof) return LDT_IMG_NOT_JPEG;
+      const int ns = s[0];
+      if (ns < 1 || ns > 4 || e - s < 4 + 2 * ns) return LDT_IMG_NOT_JPEG;
+      if (ns != H.ncomp) return LDT_IMG_UNSUPPORTED; // multi-scan sequential
+      for (int k = 0; k < ns; ++k) {
+        int idx = -1;
+        for (int c = 0; c < H.ncomp; ++c)
+          if (H.cid[c] == s[1 + 2 * k]) idx = c;
+        if (idx < 0) return LDT_IMG_NOT_JPEG;
+        H.td[idx] = s[2 + 2 * k] >> 4;
+        H.ta[idx] = s[2 + 2 * k] & 15;
+        if (H.td[idx] > 3 || H.ta[idx] > 3) return LDT_IMG_NOT_JPEG;
+      }
+      if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0)
+        return LDT_IMG_UNSUPPORTED;
+      H.scan_pos = i + seglen;
+      return LDT_IMG_OK;
+    }
+    default:
+      break;
+    }
+    i += seglen;
+  }
+}
+
+// jdhuff.c jpeg_make_d_derived_tbl restated into the device table layout.
+bool build_huff(const RawHuff &r, bool is_dc, HuffTab &t) {
+  memset(&t, 0, sizeof(t));
+  int code = 0, k = 0;
+  int lens[256];
+  int codes[256];
+  for (int l = 1; l <= 16; ++l) {
+    const int cnt = r.counts[l - 1];
+    if (cnt) {
+      t.valoff[l] = k - code;
+      for (int j = 0; j < cnt; ++j) {
+        lens[k] = l;
+        codes[k] = code;
+        ++k;
+        ++code;
+      }
+      t.maxcode[l] = code - 1;
+    } else {
+      t.maxcode[l] = -1;
+    }
+    if (cnt && code >= (1 << l)) return false; // all-ones code: JERR_BAD_HUFF_TABLE
+    code <<= 1;
+  }
+  t.maxcode[17] = 0x7FFFFFFF;
+  for (int j = 0; j < r.nsym; ++j) {
+    t.vals[j] = r.syms[j];
+    if (is_dc && r.syms[j] > 15) return false;
+  }
+  for (int j = 0; j < r.nsym; ++j) {
+    if (lens[j] <= kLookBits) {
+      const int shift = kLookBits - lens[j];
+      const int base = codes[j] << shift;
+      for (int q = 0; q < (1 << shift); ++q)
+        t.lut[base + q] = (uint16_t)((lens[j] << 8) | r.syms[j]);
+    }
+  }
+  return true;
+}
+
+std::string huff_key(const RawHuff &r, bool dc) {
+  std::string k(1, dc ? 'D' : 'A');
+  k.append(reinterpret_cast<const char *>(r.counts), 16);
+  k.append(reinterpret_cast<const char *>(r.syms), r.nsym);
+  return k;
+}
+
+inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+} // namespace
+
+// ---------------------------------------------------------------------------
+// Context.
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+
+struct PinBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+
+struct ldt_ctx {
+  int device = 0;
+  std::string err;
+  bool sync_status = true;
+  int huff_mode = 0;
+  int subseq_bits = 1024;
+  DevBuf d_data, d_plan, d_dstuf, d_coef, d_planes, d_raw;
+  static constexpr int kSlots = 2;
+  PinBuf h_data[kSlots], h_plan[kSlots];
+  hipEvent_t slot_ev[kSlots] = {nullptr, nullptr};
+  bool slot_used[kSlots] = {false, false};
+  int slot = 0;
+  int32_t *h_status = nullptr; // pinned
+  size_t h_status_cap = 0;
+  int64_t last_n = 0;
+  hipEvent_t done_ev = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool have_last = false;
+  std::unordered_map<std::string, int> hmap;
+  std::vector<HuffTab> htabs;
+  // stage profiling: one event per stage boundary, sets recycled once read
+  bool profile = false;
+  struct EvSet {
+    hipEvent_t ev[LDT_NUM_STAGES + 1];
+    int first_stage, last_stage; // stages [first, last) were recorded
+  };
+  std::vector<EvSet> ev_free, ev_pending;
+  double stage_ms[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
+  int64_t stage_cnt[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
+  EvSet *cur_ev = nullptr;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int set_err(ldt_ctx *c, int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                      \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return set_err(ctx, LDT_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));         \
+  } while (0)
+
+// Grow a device buffer; contents are not preserved. Synchronises `s` first so
+// no in-flight work still references the old allocation.
+int ensure_dev(ldt_ctx *c, DevBuf &b, size_t need, hipStream_t s) {
+  if (b.cap >= need) return LDT_OK;
+  size_t cap = need + need / 4 + 4096;
+  if (b.p) {
+    HIPCHK(c, hipStreamSynchronize(s));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  if (hipMalloc(&b.p, cap) != hipSuccess)
+    return set_err(c, LDT_ERR_NOMEM, "hipMalloc(%zu) failed", cap);
+  b.cap = cap;
+  return LDT_OK;
+}
+
+int ensure_pin(ldt_ctx *c, PinBuf &b, size_t need) {
+  if (b.cap >= need) return LDT_OK;
+  size_t cap = need + need / 4 + 4096;
+  if (b.p) {
+    HIPCHK(c, hipHostFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  if (hipHostMalloc(&b.p, cap, hipHostMallocDefault) != hipSuccess)
+    return set_err(c, LDT_ERR_NOMEM, "hipHostMalloc(%zu) failed", cap);
+  b.cap = cap;
+  return LDT_OK;
+}
+
+// Wait until the pinned slot's previous H2D copies have completed.
+int acquire_slot(ldt_ctx *c) {
+  c->slot = (c->slot + 1) % ldt_ctx::kSlots;
+  if (c->slot_used[c->slot]) HIPCHK(c, hipEventSynchronize(c->slot_ev[c->slot]));
+  return LDT_OK;
+}
+
+// Order this call after the previous one when the caller switches streams.
+int order_streams(ldt_ctx *c, hipStream_t s) {
+  if (c->have_last && c->last_stream != s) HIPCHK(c, hipStreamWaitEvent(s, c->done_ev, 0));
+  return LDT_OK;
+}
+
+int finish_call(ldt_ctx *c, hipStream_t s) {
+  HIPCHK(c, hipEventRecord(c->done_ev, s));
+  c->last_stream = s;
+  c->have_last = true;
+  return LDT_OK;
+}
+
+// ---- stage profiling helpers ----
+void prof_begin(ldt_ctx *c, int first_stage, hipStream_t s) {
+  c->cur_ev = nullptr;
+  if (!c->profile) return;
+  ldt_ctx::EvSet es;
+  if (!c->ev_free.empty()) {
+    es = c->ev_free.back();
+    c->ev_free.pop_back();
+  } else {
+    for (int k = 0; k <= LDT_NUM_STAGES; ++k)
+      if (hipEventCreate(&es.ev[k]) != hipSuccess) return;
+  }
+  es.first_stage = es.last_stage = first_stage;
+  c->ev_pending.push_back(es);
+  c->cur_ev = &c->ev_pending.back();
+  (void)hipEventRecord(c->cur_ev->ev[first_stage], s);
+}
+
+// Marks the end of `stage` (events for stages must be recorded in order).
+void prof_mark(ldt_ctx *c, int stage, hipStream_t s) {
+  if (!c->cur_ev) return;
+  (void)hipEventRecord(c->cur_ev->ev[stage + 1], s);
+  c->cur_ev->last_stage = stage + 1;
+}
+
+void build_lut(const ldt_norm *norm, float *lut) {
+  // torchvision to_tensor: float32(v) / 255 (IEEE single), then Normalize:
+  // (x - mean) / std in float32 (tensor.sub_(mean).div_(std)).
+  for (int c = 0; c < 3; ++c)
+    for (int v = 0; v < 256; ++v) {
+      volatile float x = (float)v / 255.0f;
+      if (norm) {
+        volatile float t = x - norm->mean[c];
+        x = t / norm->std[c];
+      }
+      lut[c * 256 + v] = x;
+    }
+}
+
+struct ImgPlan {
+  Header H;
+  int status = LDT_IMG_OK;
+  int64_t cell_off = 0, cell_len = 0;
+};
+
+// Core of every JPEG decode entry point.
+//   data_host: cells (host); cell i = [off(i) - base, off(i+1) - base)
+//   data_dev : if non-null, the cells already live in HBM at the same offsets.
+template <typename OffT>
+int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, const OffT *offsets,
+                int64_t arr_offset, int64_t n, const uint8_t *validity, const int64_t *labels,
+                int64_t label_offset, float *out_img, int64_t *out_lbl, const ldt_norm *norm,
+                hipStream_t s, int32_t *status_out) {
+  if (!c) return LDT_ERR_ARG;
+  if (n < 0 || (n > 0 && (!data_host || !offsets || !out_img || !status_out)))
+    return set_err(c, LDT_ERR_ARG, "bad argument (n=%lld)", (long long)n);
+  if (n == 0) return LDT_OK;
+  if (labels && !out_lbl) return set_err(c, LDT_ERR_ARG, "labels given without out_lbl");
+  DeviceGuard g(c->device);
+  int rc;
+  if ((rc = order_streams(c, s))) return rc;
+
+  // ---- parse headers ----
+  const int64_t base = (int64_t)offsets[arr_offset];
+  const int64_t total_bytes = (int64_t)offsets[arr_offset + n] - base;
+  if (total_bytes < 0) return set_err(c, LDT_ERR_ARG, "offsets not monotonic");
+  std::vector<ImgPlan> P((size_t)n);
+  std::vector<ImgDesc> D((size_t)n);
+  std::vector<Segment> S;
+  std::vector<int32_t> st((size_t)n, 0);
+  std::vector<std::vector<uint16_t>> qtabs;
+  std::unordered_map<std::string, int> qmap;
+  std::vector<int> batch_htab_ids; // ctx table id -> index in this batch
+  std::unordered_map<int, int> hid_to_batch;
+  std::vector<HuffTab> batch_htabs;
+  int64_t dst_total = 0, coef_blocks = 0, plane_total = 0, max_blocks = 0;
+  int max_w = 1, max_ks_h = 3, max_ks_v = 3;
+  bool any_bad = false;
+  for (int64_t i = 0; i < n; ++i) {
+    ImgPlan &ip = P[(size_t)i];
+    ImgDesc &d = D[(size_t)i];
+    memset(&d, 0, sizeof(d));
+    const int64_t r = arr_offset + i;
+    ip.cell_off = (int64_t)offsets[r] - base;
+    ip.cell_len = (int64_t)offsets[r + 1] - (int64_t)offsets[r];
+    d.seg_base = (int32_t)S.size();
+    if (validity && !((validity[r >> 3] >> (r & 7)) & 1)) {
+      ip.status = LDT_IMG_NULL;
+    } else if (ip.cell_len < 0) {
+      ip.status = LDT_IMG_NOT_JPEG;
+    } else {
+      ip.status = walk_markers(data_host + ip.cell_off, ip.cell_len, ip.H);
+    }
+    Header &H = ip.H;
+    if (ip.status == LDT_IMG_OK && (H.width > LDT_MAX_DIM || H.height > LDT_MAX_DIM))
+      ip.status = LDT_IMG_TOO_LARGE;
+    int hmax = 1, vmax = 1;
+    if (ip.status == LDT_IMG_OK) {
+      for (int k = 0; k < H.ncomp; ++k) {
+        if (!H.qpresent[H.tq[k]] || !H.dc[H.td[k]].present || !H.ac[H.ta[k]].present) {
+          ip.status = LDT_IMG_NOT_JPEG;
+          break;
+        }
+        hmax = H.h[k] > hmax ? H.h[k] : hmax;
+        vmax = H.v[k] > vmax ? H.v[k] : vmax;
+      }
+    }
+    if (ip.status == LDT_IMG_OK && H.ncomp == 3) {
+      // supported upsampling: every component factor divides the max, <= 2
+      int bpm = 0;
+      for (int k = 0; k < 3; ++k) {
+        if (hmax % H.h[k] || vmax % H.v[k]) ip.status = LDT_IMG_UNSUPPORTED;
+        bpm += H.h[k] * H.v[k];
+      }
+      if (bpm > kMaxBlocksPerMcu) ip.status = LDT_IMG_UNSUPPORTED;
+    }
+    if (ip.status != LDT_IMG_OK) {
+      st[(size_t)i] = ip.status;
+      any_bad = true;
+      d.width = d.height = 1;
+      d.nseg = 0;
+      continue;
+    }
+    d.width = H.width;
+    d.height = H.height;
+    d.ncomp = H.ncomp;
+    if (H.ncomp == 1) {
+      d.color = 2;
+      d.mcux = (H.width + 7) / 8;
+      d.mcuy = (H.height + 7) / 8;
+      d.bpm = 1;
+      d.bcomp[0] = 0;
+      d.ch[0] = d.cv[0] = 1;
+      d.hf[0] = d.vf[0] = 1;
+    } else {
+      // jdapimin.c default_decompress_parms: JFIF -> YCbCr; Adobe transform 0 -> RGB;
+      // otherwise component ids 'R','G','B' -> RGB; else YCbCr.
+      bool rgb;
+      if (H.jfif) rgb = false;
+      else if (H.adobe) rgb = (H.adobe_transform == 0);
+      else rgb = (H.cid[0] == 82 && H.cid[1] == 71 && H.cid[2] == 66);
+      d.color = rgb ? 1 : 0;
+      d.mcux = (H.width + 8 * hmax - 1) / (8 * hmax);
+      d.mcuy = (H.height + 8 * vmax - 1) / (8 * vmax);
+      int b = 0;
+      for (int k = 0; k < 3; ++k) {
+        d.ch[k] = H.h[k];
+        d.cv[k] = H.v[k];
+        d.hf[k] = hmax / H.h[k];
+        d.vf[k] = vmax / H.v[k];
+        for (int yy = 0; yy < H.v[k]; ++yy)
+          for (int xx = 0; xx < H.h[k]; ++xx) {
+            d.bcomp[b] = (uint8_t)k;
+            d.bdx[b] = (uint8_t)xx;
+            d.bdy[b] = (uint8_t)yy;
+            ++b;
+          }
+      }
+      d.bpm = b;
+    }
+    int64_t pl = plane_total;
+    for (int k = 0; k < H.ncomp; ++k) {
+      const int bw = d.mcux * d.ch[k], bh = d.mcuy * d.cv[k];
+      d.plane_stride[k] = bw * 8;
+      d.plane_off[k] = pl;
+      pl += align_up((int64_t)bw * 8 * bh * 8, 256);
+      d.cdw[k] = (int)(((int64_t)H.width * d.ch[k] + hmax - 1) / hmax);
+      d.cdh[k] = (int)(((int64_t)H.height * d.cv[k] + vmax - 1) / vmax);
+      if (H.ncomp == 1) {
+        d.cdw[k] = H.width;
+        d.cdh[k] = H.height;
+      }
+      // quant table
+      std::string qk(reinterpret_cast<const char *>(H.q[H.tq[k]]), 128);
+      auto qi = qmap.find(qk);
+      if (qi == qmap.end()) {
+        qi = qmap.emplace(qk, (int)qtabs.size()).first;
+        qtabs.emplace_back(H.q[H.tq[k]], H.q[H.tq[k]] + 64);
+      }
+      d.qt[k] = qi->second;
+      // Huffman tables (deduped across the context's lifetime)
+      for (int pass = 0; pass < 2; ++pass) {
+        const RawHuff &rh = pass == 0 ? H.dc[H.td[k]] : H.ac[H.ta[k]];
+        std::string key = huff_key(rh, pass == 0);
+        auto it = c->hmap.find(key);
+        int cid;
+        if (it == c->hmap.end()) {
+          HuffTab t;
+          if (!build_huff(rh, pass == 0, t)) {
+            ip.status = LDT_IMG_NOT_JPEG;
+            break;
+          }
+          cid = (int)c->htabs.size();
+          c->htabs.push_back(t);
+          c->hmap.emplace(std::move(key), cid);
+        } else {
+          cid = it->second;
+        }
+        auto bi = hid_to_batch.find(cid);
+        int bidx;
+        if (bi == hid_to_batch.end()) {
+          bidx = (int)batch_htabs.size();
+          batch_htabs.push_back(c->htabs[(size_t)cid]);
+          hid_to_batch.emplace(cid, bidx);
+        } else {
+          bidx = bi->second;
+        }
+        if (pass == 0) d.dct[k] = bidx;
+        else d.act[k] = bidx;
+      }
+    }
+    if (ip.status != LDT_IMG_OK) {
+      st[(size_t)i] = ip.status;
+      any_bad = true;
+      d.nseg = 0;
+      d.width = d.height = 1;
+      continue;
+    }
+    plane_total = pl;
+    d.restart = H.restart;
+    const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
+    d.nseg = H.restart ? (int32_t)((nmcu + H.restart - 1) / H.restart) : 1;
+    for (int sidx = 0; sidx < d.nseg; ++sidx) {
+      Segment sg;
+      memset(&sg, 0, sizeof(sg));
+      sg.img = (int32_t)i;
+      sg.mcu_first = H.restart ? sidx * H.restart : 0;
+      sg.mcu_count = H.restart ? (int32_t)std::min<int64_t>(H.restart, nmcu - sg.mcu_first)
+                               : (int32_t)nmcu;
+      S.push_back(sg);
+    }
+    d.src_off = ip.cell_off + H.scan_pos;
+    d.src_len = ip.cell_len - H.scan_pos;
+    d.dst_off = dst_total;
+    dst_total += align_up(d.src_len + 16, 16);
+    d.coef_off = coef_blocks;
+    const int64_t nblk = nmcu * d.bpm;
+    coef_blocks += nblk;
+    if (nblk > max_blocks) max_blocks = nblk;
+    if (H.width > max_w) max_w = H.width;
+    int kh = resample_ksize_host(H.width, kOut), kv = resample_ksize_host(H.height, kOut);
+    if (kh > max_ks_h) max_ks_h = kh;
+    if (kv > max_ks_v) max_ks_v = kv;
+  }
+
+  // ---- plan blob layout ----
+  PlanHdr ph;
+  memset(&ph, 0, sizeof(ph));
+  ph.n = (int32_t)n;
+  ph.nseg = (int32_t)S.size();
+  ph.nhuff = (int32_t)batch_htabs.size();
+  ph.nquant = (int32_t)qtabs.size();
+  int64_t off = align_up(sizeof(PlanHdr), 64);
+  ph.off_desc = off;
+  off = align_up(off + (int64_t)sizeof(ImgDesc) * n, 64);
+  ph.off_seg = off;
+  off = align_up(off + (int64_t)sizeof(Segment) * (int64_t)S.size(), 64);
+  ph.off_huff = off;
+  off = align_up(off + (int64_t)sizeof(HuffTab) * (int64_t)batch_htabs.size(), 64);
+  ph.off_quant = off;
+  off = align_up(off + 128 * (int64_t)qtabs.size(), 64);
+  ph.off_lut = off;
+  off = align_up(off + 3 * 256 * 4, 64);
+  ph.off_labels = off;
+  off = align_up(off + (labels ? 8 * n : 0), 64);
+  const int64_t off_status = off;
+  off = align_up(off + 4 * n, 64);
+  const int64_t plan_bytes = off;
+  ph.has_labels = labels ? 1 : 0;
+  ph.max_ks_h = max_ks_h;
+  ph.max_ks_v = max_ks_v;
+  ph.max_w = max_w;
+  ph.max_blocks = max_blocks;
+  ph.total_blocks = coef_blocks;
+
+  if ((rc = acquire_slot(c))) return rc;
+  const int sl = c->slot;
+  if ((rc = ensure_pin(c, c->h_plan[sl], (size_t)plan_bytes))) return rc;
+  uint8_t *hp = static_cast<uint8_t *>(c->h_plan[sl].p);
+  memcpy(hp, &ph, sizeof(ph));
+  memcpy(hp + ph.off_desc, D.data(), sizeof(ImgDesc) * (size_t)n);
+  if (!S.empty()) memcpy(hp + ph.off_seg, S.data(), sizeof(Segment) * S.size());
+  if (!batch_htabs.empty())
+    memcpy(hp + ph.off_huff, batch_htabs.data(), sizeof(HuffTab) * batch_htabs.size());
+  for (size_t q = 0; q < qtabs.size(); ++q) memcpy(hp + ph.off_quant + 128 * q, qtabs[q].data(), 128);
+  build_lut(norm, reinterpret_cast<float *>(hp + ph.off_lut));
+  if (labels) memcpy(hp + ph.off_labels, labels + label_offset, 8 * (size_t)n);
+  memcpy(hp + off_status, st.data(), 4 * (size_t)n);
+
+  // ---- device workspace ----
+  if ((rc = ensure_dev(c, c->d_plan, (size_t)plan_bytes, s))) return rc;
+  if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 64, s))) return rc;
+  if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 128 + 64, s))) return rc;
+  if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
+  prof_begin(c, LDT_STAGE_H2D, s);
+  const uint8_t *dev_cells = data_dev;
+  if (!data_dev) {
+    if ((rc = ensure_pin(c, c->h_data[sl], (size_t)total_bytes + 16))) return rc;
+    if ((rc = ensure_dev(c, c->d_data, (size_t)total_bytes + 16, s))) return rc;
+    memcpy(c->h_data[sl].p, data_host, (size_t)total_bytes);
+    HIPCHK(c, hipMemcpyAsync(c->d_data.p, c->h_data[sl].p, (size_t)total_bytes,
+                             hipMemcpyHostToDevice, s));
+    dev_cells = static_cast<const uint8_t *>(c->d_data.p);
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_plan.p, hp, (size_t)plan_bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipEventRecord(c->slot_ev[sl], s));
+  c->slot_used[sl] = true;
+  prof_mark(c, LDT_STAGE_H2D, s);
+  if (coef_blocks > 0) HIPCHK(c, hipMemsetAsync(c->d_coef.p, 0, (size_t)coef_blocks * 128, s));
+
+  uint8_t *dp = static_cast<uint8_t *>(c->d_plan.p);
+  DevPlan p;
+  p.descs = reinterpret_cast<const ImgDesc *>(dp + ph.off_desc);
+  p.segs = reinterpret_cast<Segment *>(dp + ph.off_seg);
+  p.htabs = reinterpret_cast<const HuffTab *>(dp + ph.off_huff);
+  p.qtabs = reinterpret_cast<const uint16_t *>(dp + ph.off_quant);
+  p.lut = reinterpret_cast<const float *>(dp + ph.off_lut);
+  p.labels = labels ? reinterpret_cast<const int64_t *>(dp + ph.off_labels) : nullptr;
+  p.n = (int)n;
+  p.nseg = (int)S.size();
+  p.max_ks_h = max_ks_h;
+  p.max_ks_v = max_ks_v;
+  p.max_w = max_w;
+  p.max_blocks = max_blocks;
+  DevWork w;
+  w.data = dev_cells;
+  w.dstuf = static_cast<uint8_t *>(c->d_dstuf.p);
+  w.coef = static_cast<int16_t *>(c->d_coef.p);
+  w.planes = static_cast<uint8_t *>(c->d_planes.p);
+  w.status = reinterpret_cast<int32_t *>(dp + off_status);
+
+  HIPCHK(c, launch_destuff(p, w, s));
+  prof_mark(c, LDT_STAGE_DESTUFF, s);
+  HIPCHK(c, launch_huff_serial(p, w, s));
+  prof_mark(c, LDT_STAGE_HUFFMAN, s);
+  HIPCHK(c, launch_idct(p, w, s));
+  prof_mark(c, LDT_STAGE_IDCT, s);
+  HIPCHK(c, launch_resize_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s));
+  prof_mark(c, LDT_STAGE_RESIZE, s);
+  c->cur_ev = nullptr;
+
+  // ---- per-image status back to the host ----
+  if ((size_t)n > c->h_status_cap) {
+    if (c->h_status) HIPCHK(c, hipHostFree(c->h_status));
+    c->h_status = nullptr;
+    if (hipHostMalloc((void **)&c->h_status, 4 * (size_t)n, hipHostMallocDefault) != hipSuccess)
+      return set_err(c, LDT_ERR_NOMEM, "hipHostMalloc(status) failed");
+    c->h_status_cap = (size_t)n;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->h_status, w.status, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  c->last_n = n;
+  if ((rc = finish_call(c, s))) return rc;
+  memcpy(status_out, st.data(), 4 * (size_t)n);
+  if (c->sync_status) {
+    HIPCHK(c, hipStreamSynchronize(s));
+    bool bad = false;
+    for (int64_t i = 0; i < n; ++i) {
+      if (status_out[i] == 0) status_out[i] = c->h_status[i];
+      if (status_out[i]) bad = true;
+    }
+    if (bad) return set_err(c, LDT_ERR_IMAGE, "one or more images failed to decode");
+  } else if (any_bad) {
+    return set_err(c, LDT_ERR_IMAGE, "one or more images failed to parse");
+  }
+  return LDT_OK;
+}
+
+} // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI.
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char *ldt_version(void) { return "ldt 0.1.0 gfx950"; }
+
+ldt_ctx *ldt_create(int device, size_t max_batch_bytes, int max_n) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+  ldt_ctx *c = new (std::nothrow) ldt_ctx();
+  if (!c) return nullptr;
+  c->device = device;
+  DeviceGuard g(device);
+  for (int k = 0; k < ldt_ctx::kSlots; ++k)
+    if (hipEventCreateWithFlags(&c->slot_ev[k], hipEventDisableTiming) != hipSuccess) {
+      delete c;
+      return nullptr;
+    }
+  if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  if (max_batch_bytes > 0) {
+    (void)ensure_dev(c, c->d_data, max_batch_bytes, nullptr);
+    for (int k = 0; k < ldt_ctx::kSlots; ++k) (void)ensure_pin(c, c->h_data[k], max_batch_bytes);
+  }
+  (void)max_n;
+  return c;
+}
+
+void ldt_destroy(ldt_ctx *c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  (void)hipDeviceSynchronize();
+  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_planes, &c->d_raw};
+  for (DevBuf *b : dbs)
+    if (b->p) (void)hipFree(b->p);
+  for (int k = 0; k < ldt_ctx::kSlots; ++k) {
+    if (c->h_data[k].p) (void)hipHostFree(c->h_data[k].p);
+    if (c->h_plan[k].p) (void)hipHostFree(c->h_plan[k].p);
+    if (c->slot_ev[k]) (void)hipEventDestroy(c->slot_ev[k]);
+  }
+  if (c->h_status) (void)hipHostFree(c->h_status);
+  if (c->done_ev) (void)hipEventDestroy(c->done_ev);
+  delete c;
+}
+
+const char *ldt_last_error(ldt_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
+  if (!c) return LDT_ERR_ARG;
+  switch (option) {
+  case LDT_OPT_SYNC_STATUS:
+    c->sync_status = value != 0;
+    return LDT_OK;
+  case LDT_OPT_HUFF_MODE:
+    if (value < 0 || value > 2) return set_err(c, LDT_ERR_ARG, "huff mode %lld", (long long)value);
+    c->huff_mode = (int)value;
+    return LDT_OK;
+  case LDT_OPT_PROFILE:
+    c->profile = value != 0;
+    return LDT_OK;
+  case LDT_OPT_SUBSEQ_BITS:
+    if (value < 64 || value > (1 << 20) || (value & 31))
+      return set_err(c, LDT_ERR_ARG, "subsequence bits %lld", (long long)value);
+    c->subseq_bits = (int)value;
+    return LDT_OK;
+  default:
+    return set_err(c, LDT_ERR_ARG, "unknown option %d", option);
+  }
+}
+
+int ldt_decode_batch(ldt_ctx *c, const uint8_t *data, const int32_t *offsets, int64_t arr_offset,
+                     int64_t n, const uint8_t *validity, const int64_t *labels,
+                     int64_t label_offset, float *out_img_dev, int64_t *out_lbl_dev,
+                     const ldt_norm *norm, void *stream, int32_t *per_image_status) {
+  return decode_core<int32_t>(c, data, nullptr, offsets, arr_offset, n, validity, labels,
+                              label_offset, out_img_dev, out_lbl_dev, norm, (hipStream_t)stream,
+                              per_image_status);
+}
+
+int ldt_decode_batch_large(ldt_ctx *c, const uint8_t *data, const int64_t *offsets,
+                           int64_t arr_offset, int64_t n, const uint8_t *validity,
+                           const int64_t *labels, int64_t label_offset, float *out_img_dev,
+                           int64_t *out_lbl_dev, const ldt_norm *norm, void *stream,
+                           int32_t *per_image_status) {
+  return decode_core<int64_t>(c, data, nullptr, offsets, arr_offset, n, validity, labels,
+                              label_offset, out_img_dev, out_lbl_dev, norm, (hipStream_t)stream,
+                              per_image_status);
+}
+
+int ldt_decode_batch_resident(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev,
+                              const int64_t *offsets, int64_t n, const int64_t *labels,
+                              float *out_img_dev, int64_t *out_lbl_dev, const ldt_norm *norm,
+                              void *stream, int32_t *per_image_status) {
+  if (!data_dev) return set_err(c, LDT_ERR_ARG, "data_dev is null");
+  if (c && n > 0 && offsets[0] != 0)
+    return set_err(c, LDT_ERR_ARG, "resident offsets must start at 0");
+  return decode_core<int64_t>(c, data_host, data_dev, offsets, 0, n, nullptr, labels, 0,
+                              out_img_dev, out_lbl_dev, norm, (hipStream_t)stream,
+                              per_image_status);
+}
+
+int ldt_stage_times(ldt_ctx *c, double *ms_out, int64_t *count_out, int reset) {
+  if (!c) return LDT_ERR_ARG;
+  DeviceGuard g(c->device);
+  for (auto &es : c->ev_pending) {
+    HIPCHK(c, hipEventSynchronize(es.ev[es.last_stage]));
+    for (int k = es.first_stage; k < es.last_stage; ++k) {
+      float ms = 0.f;
+      HIPCHK(c, hipEventElapsedTime(&ms, es.ev[k], es.ev[k + 1]));
+      c->stage_ms[k] += ms;
+      c->stage_cnt[k] += 1;
+    }
+    c->ev_free.push_back(es);
+  }
+  c->ev_pending.clear();
+  for (int k = 0; k < LDT_NUM_STAGES; ++k) {
+    if (ms_out) ms_out[k] = c->stage_ms[k];
+    if (count_out) count_out[k] = c->stage_cnt[k];
+    if (reset) {
+      c->stage_ms[k] = 0;
+      c->stage_cnt[k] = 0;
+    }
+  }
+  return LDT_OK;
+}
+
+int ldt_fetch_status(ldt_ctx *c, void *stream, int32_t *st, int64_t n) {
+  if (!c || !st) return LDT_ERR_ARG;
+  DeviceGuard g(c->device);
+  HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+  if (n > c->last_n) return set_err(c, LDT_ERR_ARG, "n exceeds last batch");
+  bool bad = false;
+  for (int64_t i = 0; i < n; ++i) {
+    if (st[i] == 0) st[i] = c->h_status[i];
+    if (st[i]) bad = true;
+  }
+  return bad ? set_err(c, LDT_ERR_IMAGE, "one or more images failed to decode") : LDT_OK;
+}
+
+int ldt_resize_raw(ldt_ctx *c, const uint8_t *hwc, int hwc_is_device, int64_t n, int h, int w,
+                   int64_t cell_stride, float *out_img_dev, const ldt_norm *norm, void *stream) {
+  if (!c) return LDT_ERR_ARG;
+  if (n < 0 || h <= 0 || w <= 0 || h > LDT_MAX_DIM || w > LDT_MAX_DIM || !out_img_dev ||
+      (n > 0 && !hwc) || cell_stride < (int64_t)h * w * 3)
+    return set_err(c, LDT_ERR_ARG, "bad raw resize arguments");
+  if (n == 0) return LDT_OK;
+  DeviceGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = order_streams(c, s))) return rc;
+  if ((rc = acquire_slot(c))) return rc;
+  const int sl = c->slot;
+  if ((rc = ensure_pin(c, c->h_plan[sl], 3 * 256 * 4))) return rc;
+  float *hl = static_cast<float *>(c->h_plan[sl].p);
+  build_lut(norm, hl);
+  if ((rc = ensure_dev(c, c->d_plan, 3 * 256 * 4, s))) return rc;
+  const uint8_t *src = hwc;
+  if (!hwc_is_device) {
+    const size_t bytes = (size_t)(cell_stride * (n - 1) + (int64_t)h * w * 3);
+    if ((rc = ensure_pin(c, c->h_data[sl], bytes))) return rc;
+    if ((rc = ensure_dev(c, c->d_raw, bytes, s))) return rc;
+    memcpy(c->h_data[sl].p, hwc, bytes);
+    HIPCHK(c, hipMemcpyAsync(c->d_raw.p, c->h_data[sl].p, bytes, hipMemcpyHostToDevice, s));
+    src = static_cast<const uint8_t *>(c->d_raw.p);
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_plan.p, hl, 3 * 256 * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipEventRecord(c->slot_ev[sl], s));
+  c->slot_used[sl] = true;
+  prof_begin(c, LDT_STAGE_RESIZE, s);
+  HIPCHK(c, launch_resize_raw(src, cell_stride, (int)n, h, w,
+                              static_cast<const float *>(c->d_plan.p), out_img_dev, s));
+  prof_mark(c, LDT_STAGE_RESIZE, s);
+  c->cur_ev = nullptr;
+  if ((rc = finish_call(c, s))) return rc;
+  if (c->sync_status) HIPCHK(c, hipStreamSynchronize(s));
+  return LDT_OK;
+}
+
+int ldt_shard_ranges(ldt_ctx *c, int64_t num_rows, int64_t batch_size, int rank, int world_size,
+                     int64_t *out_ranges_dev, int64_t capacity, int64_t *out_count_dev,
+                     void *stream) {
+  if (!c) return LDT_ERR_ARG;
+  if (num_rows < 0 || batch_size <= 0 || world_size <= 0 || rank < 0 || rank >= world_size ||
+      !out_count_dev || (capacity > 0 && !out_ranges_dev))
+    return set_err(c, LDT_ERR_ARG, "bad shard_ranges arguments");
+  DeviceGuard g(c->device);
+  HIPCHK(c, launch_shard_ranges(num_rows, batch_size, rank, world_size, out_ranges_dev, capacity,
+                                out_count_dev, (hipStream_t)stream));
+  return LDT_OK;
+}
+
+int ldt_shard_fragments(ldt_ctx *c, const int64_t *fragment_rows_dev, int nfrag,
+                        int64_t batch_size, int rank, int world_size, int64_t pad_to,
+                        int64_t *out_dev, int64_t capacity, int64_t *out_count_dev,
+                        int64_t *out_local_count_dev, void *stream) {
+  if (!c) return LDT_ERR_ARG;
+  if (nfrag < 0 || batch_size <= 0 || world_size <= 0 || rank < 0 || rank >= world_size ||
+      !out_count_dev || !out_local_count_dev || (nfrag > 0 && !fragment_rows_dev) ||
+      (capacity > 0 && !out_dev))
+    return set_err(c, LDT_ERR_ARG, "bad shard_fragments arguments");
+  DeviceGuard g(c->device);
+  HIPCHK(c, launch_shard_fragments(fragment_rows_dev, nfrag, batch_size, rank, world_size, pad_to,
+                                   out_dev, capacity, out_count_dev, out_local_count_dev,
+                                   (hipStream_t)stream));
+  return LDT_OK;
+}
+
+// Test hook (not part of ldt.h's stable surface): Pillow resample coefficient
+// tables computed on the device, for parity tests against the oracle.
+int ldt_debug_resample_coeffs(ldt_ctx *c, int in_size, int out_size, int32_t *bounds_dev,
+                              int32_t *kk_dev, void *stream) {
+  if (!c) return LDT_ERR_ARG;
+  DeviceGuard g(c->device);
+  HIPCHK(c, launch_resample_coeffs(in_size, out_size, resample_ksize_host(in_size, out_size),
+                                   bounds_dev, kk_dev, (hipStream_t)stream));
+  return LDT_OK;
+}
+
+} // extern "C"

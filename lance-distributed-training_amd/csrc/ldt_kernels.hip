@@ -1,0 +1,781 @@
+// ldt_kernels.hip — gfx950 (MI355X / CDNA4) kernels of the batch-decode path.
+//
+// Pipeline per batch (all device-resident, one HIP stream):
+//   k_destuff     one workgroup per image: remove 0xFF00 stuffing, split the
+//                 entropy-coded data at RSTn markers into segments, find the
+//                 end-of-scan marker (libjpeg jdmarker.c / jdhuff.c semantics).
+//   k_huff_*      baseline Huffman decode of each segment into int16 DCT
+//                 coefficients, natural order, MCU-major block layout
+//                 (jdhuff.c decode_mcu restated; see ldt_huffman.hip).
+//   k_idct        dequantise + JDCT_ISLOW 8x8 IDCT (jidctint.c), 8 lanes per
+//                 block, column/row passes staged through LDS, uint8 planes.
+//   k_resize<S>   fused chroma fancy-upsampling (jdsample.c) + YCbCr->RGB
+//                 (jdcolor.c) + Pillow BILINEAR Resize((224,224)) (Resample.c,
+//                 22-bit fixed point, horizontal-then-vertical, uint8
+//                 intermediate) + ToTensor/Normalize via a float32 LUT, coalesced
+//                 CHW fp32 stores. S = raw HWC source for config 5.
+//   k_shard_*     ShardedBatchSampler / ShardedFragmentSampler index ranges.
+//
+// Reference call sites replaced: lance_iterable.py:38-50, lance_map_style.py:21-44,
+// lance_iterable.py:61-69. Nothing here is a dense contraction, so no MFMA: the
+// decode stages are VALU/LDS/latency bound and the resize/store is HBM bound.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ldt_kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace ldt {
+
+// ---------------------------------------------------------------------------
+// Block-wide exclusive scan (256 threads = 4 waves of 64).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// Returns the exclusive prefix of v over the block; *total = block sum.
+// `scratch` must hold >= 5 ints; contains a __syncthreads.
+__device__ __forceinline__ int block_excl_scan256(int v, int *scratch, int *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int inc = wave_incl_scan(v);
+  if (lane == 63) scratch[wave] = inc;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    int s = scratch[w];
+    if (w < wave) base += s;
+    tot += s;
+  }
+  *total = tot;
+  __syncthreads();
+  return base + inc - v;
+}
+
+// ---------------------------------------------------------------------------
+// k_destuff: one 256-thread workgroup per image, 16 bytes per thread per pass.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_destuff(const uint8_t *__restrict__ data,
+                                                 const ImgDesc *__restrict__ descs,
+                                                 Segment *__restrict__ segs,
+                                                 uint8_t *__restrict__ dst,
+                                                 int32_t *__restrict__ status) {
+  const int img = blockIdx.x;
+  const ImgDesc &d = descs[img];
+  if (status[img] != 0) return;
+  __shared__ int sh_scan[8];
+  __shared__ int sh_end;
+  const int tid = threadIdx.x;
+  const uint8_t *src = data + d.src_off;
+  const int64_t L = d.src_len;
+  uint8_t *out = dst + d.dst_off;
+  int64_t out_base = 0;   // kept bytes so far
+  int rst_base = 0;       // RST markers so far
+  bool done = false;
+  for (int64_t chunk = 0; chunk < L && !done; chunk += 256 * 16) {
+    const int64_t p0 = chunk + (int64_t)tid * 16;
+    uint8_t b[18];
+    // b[0] = byte before p0, b[1..16] = bytes p0..p0+15, b[17] = byte after
+#pragma unroll
+    for (int j = 0; j < 18; ++j) {
+      int64_t p = p0 - 1 + j;
+      b[j] = (p >= 0 && p < L) ? src[p] : 0;
+    }
+    uint32_t keep = 0, rst = 0;
+    int local_end = 16;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t p = p0 + j;
+      const uint8_t prev = b[j], cur = b[j + 1], next = b[j + 2];
+      bool in = p < L;
+      bool drop = false;
+      if (cur == 0xFF) {
+        if (next == 0x00) {
+          drop = false;                       // stuffed data byte 0xFF
+        } else if (next == 0xFF || (next >= 0xD0 && next <= 0xD7)) {
+          drop = true;                        // fill byte or RSTn prefix
+        } else if (in && p + 1 < L) {
+          if (local_end == 16) local_end = j; // end-of-scan marker
+          drop = true;
+        } else {
+          drop = true;                        // trailing 0xFF at end of cell
+        }
+      } else if (prev == 0xFF && p > 0) {
+        if (cur == 0x00) drop = true;         // stuffing zero
+        else if (cur >= 0xD0 && cur <= 0xD7) {
+          drop = true;
+          if (in) rst |= 1u << j;             // RSTn code: segment boundary
+        }
+      }
+      if (in && !drop) keep |= 1u << j;
+    }
+    if (tid == 0) sh_end = 256 * 16;
+    __syncthreads();
+    if (local_end < 16) atomicMin(&sh_end, tid * 16 + local_end);
+    __syncthreads();
+    const int cend = sh_end;
+    if (cend < 256 * 16) done = true;
+    const int my_lo = tid * 16;
+    uint32_t lim = (cend <= my_lo) ? 0u : (cend - my_lo >= 16 ? 0xFFFFu : ((1u << (cend - my_lo)) - 1u));
+    keep &= lim;
+    rst &= lim;
+    int ktot, rtot;
+    int kex = block_excl_scan256(__popc(keep), sh_scan, &ktot);
+    int rex = block_excl_scan256(__popc(rst), sh_scan, &rtot);
+    int64_t o = out_base + kex;
+    int r = rst_base + rex;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (rst & (1u << j)) {
+        ++r;
+        if (r < d.nseg) segs[d.seg_base + r].byte_start = d.dst_off + o;
+      }
+      if (keep & (1u << j)) out[o++] = b[j + 1];
+    }
+    out_base += ktot;
+    rst_base += rtot;
+  }
+  if (tid == 0) {
+    segs[d.seg_base].byte_start = d.dst_off;
+    if (rst_base != d.nseg - 1) {
+      status[img] = 3; // LDT_IMG_CORRUPT: restart markers do not match the header
+    }
+    // pad 8 zero bytes after the data so aligned 32-bit reads never see stale bytes
+    for (int j = 0; j < 8; ++j) out[out_base + j] = 0;
+  }
+  __syncthreads();
+  // segment ends: next segment's start, last = total kept bytes
+  for (int s = tid; s < d.nseg; s += 256) {
+    int64_t e = (s + 1 < d.nseg && rst_base == d.nseg - 1) ? segs[d.seg_base + s + 1].byte_start
+                                                           : d.dst_off + out_base;
+    if (rst_base != d.nseg - 1) segs[d.seg_base + s].byte_start = d.dst_off;
+    segs[d.seg_base + s].byte_end = e;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_idct: jidctint.c jpeg_idct_islow. 8 lanes per block (lane = row/column),
+// 32 blocks per 256-thread workgroup. LDS stride 72 dwords per block keeps
+// the column pass conflict-free.
+// ---------------------------------------------------------------------------
+#define FIX_0_298631336 2446
+#define FIX_0_390180644 3196
+#define FIX_0_541196100 4433
+#define FIX_0_765366865 6270
+#define FIX_0_899976223 7373
+#define FIX_1_175875602 9633
+#define FIX_1_501321110 12299
+#define FIX_1_847759065 15137
+#define FIX_1_961570560 16069
+#define FIX_2_053119869 16819
+#define FIX_2_562915447 20995
+#define FIX_3_072711026 25172
+
+// One 1-D ISLOW butterfly on in[0..7] (stride 1), producing the 8 pre-descale
+// sums in the order libjpeg stores them.
+struct Islow8 {
+  int32_t o[8];
+};
+__device__ __forceinline__ Islow8 islow_1d(const int32_t *x, int pass1) {
+  int32_t tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13, z1, z2, z3, z4, z5;
+  z2 = x[2];
+  z3 = x[6];
+  z1 = (z2 + z3) * FIX_0_541196100;
+  tmp2 = z1 + z3 * (-FIX_1_847759065);
+  tmp3 = z1 + z2 * FIX_0_765366865;
+  tmp0 = (x[0] + x[4]) * (1 << 13);
+  tmp1 = (x[0] - x[4]) * (1 << 13);
+  tmp10 = tmp0 + tmp3;
+  tmp13 = tmp0 - tmp3;
+  tmp11 = tmp1 + tmp2;
+  tmp12 = tmp1 - tmp2;
+  tmp0 = x[7];
+  tmp1 = x[5];
+  tmp2 = x[3];
+  tmp3 = x[1];
+  z1 = tmp0 + tmp3;
+  z2 = tmp1 + tmp2;
+  z3 = tmp0 + tmp2;
+  z4 = tmp1 + tmp3;
+  z5 = (z3 + z4) * FIX_1_175875602;
+  tmp0 = tmp0 * FIX_0_298631336;
+  tmp1 = tmp1 * FIX_2_053119869;
+  tmp2 = tmp2 * FIX_3_072711026;
+  tmp3 = tmp3 * FIX_1_501321110;
+  z1 = z1 * (-FIX_0_899976223);
+  z2 = z2 * (-FIX_2_562915447);
+  z3 = z3 * (-FIX_1_961570560);
+  z4 = z4 * (-FIX_0_390180644);
+  z3 += z5;
+  z4 += z5;
+  tmp0 += z1 + z3;
+  tmp1 += z2 + z4;
+  tmp2 += z2 + z3;
+  tmp3 += z1 + z4;
+  Islow8 r;
+  r.o[0] = tmp10 + tmp3;
+  r.o[7] = tmp10 - tmp3;
+  r.o[1] = tmp11 + tmp2;
+  r.o[6] = tmp11 - tmp2;
+  r.o[2] = tmp12 + tmp1;
+  r.o[5] = tmp12 - tmp1;
+  r.o[3] = tmp13 + tmp0;
+  r.o[4] = tmp13 - tmp0;
+  (void)pass1;
+  return r;
+}
+
+// jdmaster.c prepare_range_limit_table, post-IDCT part, indexed by x & 1023.
+__device__ __forceinline__ uint32_t idct_limit(int32_t x) {
+  int i = x & 1023;
+  return i < 128 ? (uint32_t)(i + 128) : (i < 512 ? 255u : (i < 896 ? 0u : (uint32_t)(i - 896)));
+}
+
+__global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
+                                              const uint16_t *__restrict__ qtabs,
+                                              const int16_t *__restrict__ coef,
+                                              uint8_t *__restrict__ planes,
+                                              const int32_t *__restrict__ status) {
+  __shared__ int32_t ws[4][8 * 72];
+  const int img = blockIdx.y;
+  if (status[img] != 0) return;
+  const ImgDesc &d = descs[img];
+  const int64_t nblk = (int64_t)d.mcux * d.mcuy * d.bpm;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bl = lane >> 3, r = lane & 7;
+  const int64_t blk = (int64_t)blockIdx.x * 32 + wave * 8 + bl;
+  if ((int64_t)blockIdx.x * 32 >= nblk) return;
+  const bool valid = blk < nblk;
+  int32_t *w = &ws[wave][bl * 72];
+  int comp = 0;
+  int64_t m = 0;
+  int b = 0;
+  if (valid) {
+    m = blk / d.bpm;
+    b = (int)(blk - m * d.bpm);
+    comp = d.bcomp[b];
+    // row r of the block: 8 int16 = 16 bytes, coalesced across the wave
+    const int4 raw = *reinterpret_cast<const int4 *>(coef + (d.coef_off + blk) * 64 + r * 8);
+    const uint4 q4 = *reinterpret_cast<const uint4 *>(qtabs + d.qt[comp] * 64 + r * 8);
+    const int16_t *cv = reinterpret_cast<const int16_t *>(&raw);
+    const uint16_t *qv = reinterpret_cast<const uint16_t *>(&q4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[r * 8 + j] = (int32_t)cv[j] * (int32_t)qv[j];
+  }
+  __syncthreads();
+  // pass 1: column r of the block (jidctint.c pass 1, with the DC shortcut)
+  if (valid) {
+    int32_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = w[j * 8 + r];
+    int32_t o[8];
+    if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = x[0] * (1 << 2);
+    } else {
+      Islow8 t = islow_1d(x, 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (t.o[j] + (1 << 10)) >> 11; // DESCALE(, 13-2)
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j * 8 + r] = o[j];
+  }
+  __syncthreads();
+  if (!valid) return;
+  // pass 2: row r
+  int32_t x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = w[r * 8 + j];
+  uint32_t px[8];
+  if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
+    const uint32_t v = idct_limit((x[0] + (1 << 4)) >> 5); // DESCALE(, PASS1_BITS+3)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) px[j] = v;
+  } else {
+    Islow8 t = islow_1d(x, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) px[j] = idct_limit((t.o[j] + (1 << 17)) >> 18); // DESCALE(, 13+2+3)
+  }
+  const int mx = (int)(m % d.mcux), my = (int)(m / d.mcux);
+  const int bx = mx * d.ch[comp] + d.bdx[b];
+  const int by = my * d.cv[comp] + d.bdy[b];
+  uint8_t *dstp = planes + d.plane_off[comp] + (int64_t)(by * 8 + r) * d.plane_stride[comp] + bx * 8;
+  uint2 packed;
+  packed.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+  packed.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
+  *reinterpret_cast<uint2 *>(dstp) = packed;
+}
+
+// ---------------------------------------------------------------------------
+// Pillow Resample.c precompute_coeffs + normalize_coeffs_8bpc for one output
+// index, BILINEAR (support 1.0), box (0, in). IEEE double, no contraction, so
+// the result equals the x86-64 build of Pillow bit for bit.
+// ---------------------------------------------------------------------------
+__device__ int resample_coeffs_one(int inSize, int outSize, int xx, int ksize, int32_t *k,
+                                   int *xmin_out) {
+#pragma clang fp contract(off)
+  const double scale = (double)inSize / (double)outSize;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 1.0 * filterscale;
+  const double center = (xx + 0.5) * scale;
+  const double ss = 1.0 / filterscale;
+  int xmin = (int)(center - support + 0.5);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(center + support + 0.5);
+  if (xmax > inSize) xmax = inSize;
+  xmax -= xmin;
+  double ww = 0.0;
+  for (int x = 0; x < xmax; ++x) {
+    double t = ((double)(x + xmin) - center + 0.5) * ss;
+    if (t < 0.0) t = -t;
+    double wv = t < 1.0 ? 1.0 - t : 0.0;
+    ww += wv;
+  }
+  for (int x = 0; x < ksize; ++x) {
+    double wv = 0.0;
+    if (x < xmax) {
+      double t = ((double)(x + xmin) - center + 0.5) * ss;
+      if (t < 0.0) t = -t;
+      wv = t < 1.0 ? 1.0 - t : 0.0;
+      if (ww != 0.0) wv = wv / ww;
+    }
+    const double v = wv * (double)(1 << kPrecisionBits);
+    k[x] = (int32_t)(wv < 0 ? (-0.5 + v) : (0.5 + v));
+  }
+  *xmin_out = xmin;
+  return xmax;
+}
+
+// Test hook: coefficient tables for one (in, out) pair.
+__global__ void k_resample_coeffs(int inSize, int outSize, int ksize, int32_t *bounds,
+                                  int32_t *kk) {
+  int xx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (xx >= outSize) return;
+  int xmin;
+  int cnt = resample_coeffs_one(inSize, outSize, xx, ksize, kk + (int64_t)xx * ksize, &xmin);
+  bounds[2 * xx] = xmin;
+  bounds[2 * xx + 1] = cnt;
+}
+
+__device__ __forceinline__ uint32_t clip8(int32_t in) {
+  if (in >= (1 << kPrecisionBits << 8)) return 255;
+  if (in <= 0) return 0;
+  return (uint32_t)(in >> kPrecisionBits);
+}
+
+// ---------------------------------------------------------------------------
+// Source-row staging for the resize kernel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// jdsample.c fancy upsampling value of chroma component c at full-res (x, y).
+__device__ __forceinline__ int chroma_at(const ImgDesc &d, const uint8_t *pl, int c, int x, int y) {
+  const int stride = d.plane_stride[c];
+  const int hf = d.hf[c], vf = d.vf[c];
+  if (hf == 1 && vf == 1) return pl[(int64_t)y * stride + x];
+  const int dw = d.cdw[c], dh = d.cdh[c];
+  if (hf == 2 && vf == 2) {
+    const int cx = x >> 1, cy = y >> 1;
+    if (dw <= 2) return pl[(int64_t)cy * stride + cx];
+    const int ny = (y & 1) ? min(cy + 1, dh - 1) : max(cy - 1, 0);
+    const int nx = (x & 1) ? min(cx + 1, dw - 1) : max(cx - 1, 0);
+    const uint8_t *r0 = pl + (int64_t)cy * stride, *r1 = pl + (int64_t)ny * stride;
+    const int thiscol = r0[cx] * 3 + r1[cx];
+    const int nextcol = r0[nx] * 3 + r1[nx];
+    return (thiscol * 3 + nextcol + 8 - (x & 1)) >> 4;
+  }
+  if (hf == 2 && vf == 1) {
+    const int cx = x >> 1;
+    const uint8_t *r0 = pl + (int64_t)y * stride;
+    if (dw <= 2) return r0[cx];
+    const int nx = (x & 1) ? min(cx + 1, dw - 1) : max(cx - 1, 0);
+    return (r0[cx] * 3 + r0[nx] + 1 + (x & 1)) >> 2;
+  }
+  return pl[(int64_t)(y / vf) * stride + (x / hf)];
+}
+
+// jdcolor.c ycc_rgb_convert with the 16-bit fixed-point tables evaluated inline.
+__device__ __forceinline__ void ycc_to_rgb(int Y, int cb, int cr, uint8_t *o) {
+  const int xcr = cr - 128, xcb = cb - 128;
+  const int cr_r = (91881 * xcr + 32768) >> 16;         // FIX(1.40200)
+  const int cb_b = (116130 * xcb + 32768) >> 16;        // FIX(1.77200)
+  const int g = (-22554 * xcb + 32768 + (-46802) * xcr) >> 16; // FIX(0.34414), FIX(0.71414)
+  o[0] = (uint8_t)clampi(Y + cr_r, 0, 255);
+  o[1] = (uint8_t)clampi(Y + g, 0, 255);
+  o[2] = (uint8_t)clampi(Y + cb_b, 0, 255);
+}
+
+// ---------------------------------------------------------------------------
+// k_resize: fused source (JPEG planes or raw HWC) -> Pillow BILINEAR 224x224
+// -> LUT (ToTensor [+Normalize]) -> fp32 CHW. One workgroup = kBandRows output
+// rows of one image; workgroups of an image share blockIdx % 8 (one XCD under
+// the observed round-robin placement, for L2 reuse of overlapping rows).
+// Each thread < 224 owns one output column: it computes the horizontal tap
+// sum of every needed source row and accumulates the vertical taps in
+// registers, so the uint8 intermediate never leaves the thread.
+// ---------------------------------------------------------------------------
+struct RawSrc {
+  const uint8_t *base;
+  int64_t cell_stride;
+  int h, w;
+};
+
+template <int SRC>
+__global__ void __launch_bounds__(kResizeThreads)
+    k_resize(const ImgDesc *__restrict__ descs, const uint8_t *__restrict__ planes, RawSrc raw,
+             const float *__restrict__ lut, const int64_t *__restrict__ labels,
+             float *__restrict__ out, int64_t *__restrict__ out_labels,
+             const int32_t *__restrict__ status, int n, int ks_h, int ks_v, int row_bytes) {
+  constexpr int NB = kOut / kBandRows;
+  const int L = blockIdx.x;
+  const int g = L / (8 * NB), rr = L % (8 * NB);
+  const int img = g * 8 + (rr % 8);
+  const int band = rr / 8;
+  if (img >= n) return;
+  if (SRC == 0 && status[img] != 0) return;
+  const int tid = threadIdx.x;
+  int W, H;
+  if (SRC == 0) {
+    W = descs[img].width;
+    H = descs[img].height;
+  } else {
+    W = raw.w;
+    H = raw.h;
+  }
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  float *s_lut = reinterpret_cast<float *>(smem);                 // 768 floats
+  int32_t *s_kh = reinterpret_cast<int32_t *>(smem + 3072);       // 224 * ks_h
+  int32_t *s_kv = s_kh + kOut * ks_h;                             // kBandRows * ks_v
+  int32_t *s_hb = s_kv + kBandRows * ks_v;                        // 224 * 2
+  int32_t *s_vb = s_hb + 2 * kOut;                                // kBandRows * 2
+  uint8_t *s_row = reinterpret_cast<uint8_t *>(s_vb + 2 * kBandRows); // 2 * row_bytes
+
+  for (int i = tid; i < 768; i += kResizeThreads) s_lut[i] = lut[i];
+  const int oy0 = band * kBandRows;
+  if (tid < kOut) {
+    int xmin;
+    int cnt = resample_coeffs_one(W, kOut, tid, ks_h, s_kh + tid * ks_h, &xmin);
+    s_hb[2 * tid] = xmin;
+    s_hb[2 * tid + 1] = cnt;
+  } else if (tid >= kOut && tid < kOut + kBandRows) {
+    const int j = tid - kOut;
+    int ymin;
+    int cnt = resample_coeffs_one(H, kOut, oy0 + j, ks_v, s_kv + j * ks_v, &ymin);
+    s_vb[2 * j] = ymin;
+    s_vb[2 * j + 1] = cnt;
+  }
+  if (band == 0 && tid == 0 && labels != nullptr) out_labels[img] = labels[img];
+  __syncthreads();
+  const int ya = s_vb[0];
+  const int yb = s_vb[2 * (kBandRows - 1)] + s_vb[2 * (kBandRows - 1) + 1];
+
+  int32_t acc[kBandRows][3];
+#pragma unroll
+  for (int j = 0; j < kBandRows; ++j) acc[j][0] = acc[j][1] = acc[j][2] = 1 << (kPrecisionBits - 1);
+  int hxmin = 0, hcnt = 0;
+  if (tid < kOut) {
+    hxmin = s_hb[2 * tid];
+    hcnt = s_hb[2 * tid + 1];
+  }
+
+  for (int y = ya; y < yb; ++y) {
+    uint8_t *row = s_row + ((y - ya) & 1) * row_bytes;
+    // ---- stage source row y as interleaved RGB in LDS ----
+    if (SRC == 0) {
+      const ImgDesc &d = descs[img];
+      const uint8_t *py = planes + d.plane_off[0] + (int64_t)y * d.plane_stride[0];
+      if (d.color == 2) {
+        for (int x = tid; x < W; x += kResizeThreads) {
+          const uint8_t v = py[x];
+          row[3 * x] = v;
+          row[3 * x + 1] = v;
+          row[3 * x + 2] = v;
+        }
+      } else {
+        const uint8_t *pcb = planes + d.plane_off[1];
+        const uint8_t *pcr = planes + d.plane_off[2];
+        for (int x = tid; x < W; x += kResizeThreads) {
+          const int Y = py[x];
+          const int cb = chroma_at(d, pcb, 1, x, y);
+          const int cr = chroma_at(d, pcr, 2, x, y);
+          if (d.color == 1) {
+            row[3 * x] = (uint8_t)Y;
+            row[3 * x + 1] = (uint8_t)cb;
+            row[3 * x + 2] = (uint8_t)cr;
+          } else {
+            ycc_to_rgb(Y, cb, cr, row + 3 * x);
+          }
+        }
+      }
+    } else {
+      const uint8_t *src = raw.base + (int64_t)img * raw.cell_stride + (int64_t)y * W * 3;
+      const int nbytes = W * 3;
+      if ((((uintptr_t)src) & 3) == 0 && (nbytes & 3) == 0) {
+        const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src);
+        uint32_t *r4 = reinterpret_cast<uint32_t *>(row);
+        for (int i = tid; i < nbytes / 4; i += kResizeThreads) r4[i] = s4[i];
+      } else {
+        for (int i = tid; i < nbytes; i += kResizeThreads) row[i] = src[i];
+      }
+    }
+    __syncthreads();
+    // ---- horizontal taps for column tid, then vertical accumulate ----
+    if (tid < kOut) {
+      int32_t s0 = 1 << (kPrecisionBits - 1), s1 = s0, s2 = s0;
+      const int32_t *k = s_kh + tid * ks_h;
+      const uint8_t *p = row + 3 * hxmin;
+      for (int t = 0; t < hcnt; ++t) {
+        const int32_t kw = k[t];
+        s0 += (int32_t)p[3 * t] * kw;
+        s1 += (int32_t)p[3 * t + 1] * kw;
+        s2 += (int32_t)p[3 * t + 2] * kw;
+      }
+      const int32_t h0 = (int32_t)clip8(s0), h1 = (int32_t)clip8(s1), h2 = (int32_t)clip8(s2);
+#pragma unroll
+      for (int j = 0; j < kBandRows; ++j) {
+        const int jj = y - s_vb[2 * j];
+        if (jj >= 0 && jj < s_vb[2 * j + 1]) {
+          const int32_t kw = s_kv[j * ks_v + jj];
+          acc[j][0] += h0 * kw;
+          acc[j][1] += h1 * kw;
+          acc[j][2] += h2 * kw;
+        }
+      }
+    }
+    // the next iteration writes the other row buffer; one barrier per row suffices
+  }
+  if (tid < kOut) {
+    float *o = out + (int64_t)img * 3 * kOut * kOut;
+#pragma unroll
+    for (int j = 0; j < kBandRows; ++j) {
+      const int oy = oy0 + j;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) o[((int64_t)c * kOut + oy) * kOut + tid] = s_lut[c * 256 + clip8(acc[j][c])];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Samplers.
+// ---------------------------------------------------------------------------
+// ShardedBatchSampler (README.md:257-271): pairs [k*B, min(k*B+B, N)), k = r, r+W, ...
+__global__ void k_shard_ranges(int64_t num_rows, int64_t bsz, int rank, int world,
+                               int64_t *out, int64_t capacity, int64_t *count) {
+  const int64_t nb = (num_rows + bsz - 1) / bsz;
+  const int64_t cnt = rank < nb ? (nb - rank + world - 1) / world : 0;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *count = cnt;
+  if (i < cnt && i < capacity) {
+    const int64_t k = rank + i * world;
+    const int64_t s = k * bsz;
+    out[2 * i] = s;
+    out[2 * i + 1] = min(s + bsz, num_rows);
+  }
+}
+
+// ShardedFragmentSampler (README.md:140-155) + this build's pad rule.
+// Single workgroup: per-fragment batch counts, block scans over fragments
+// (global batch ids and own-rank batch ids), then record emission.
+__global__ void __launch_bounds__(256) k_shard_fragments(const int64_t *frag_rows, int nfrag,
+                                                         int64_t bsz, int rank, int world,
+                                                         int64_t pad_to, int64_t *out,
+                                                         int64_t capacity, int64_t *count,
+                                                         int64_t *local_count) {
+  __shared__ int sh_scan[8];
+  __shared__ long long sh_tot[3]; // own batches, global batches, rows
+  __shared__ long long sh_max_rank;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    sh_tot[0] = sh_tot[1] = sh_tot[2] = 0;
+    sh_max_rank = 0;
+  }
+  __syncthreads();
+  // pass 1: own records
+  for (int f0 = 0; f0 < nfrag; f0 += 256) {
+    const int f = f0 + tid;
+    int64_t rows = f < nfrag ? frag_rows[f] : 0;
+    int64_t nbf = (rows + bsz - 1) / bsz;
+    int own = (f < nfrag && (f % world) == rank) ? (int)nbf : 0;
+    int tot_own, tot_all, tot_rows_i;
+    int own_ex = block_excl_scan256(own, sh_scan, &tot_own);
+    int all_ex = block_excl_scan256((int)nbf, sh_scan, &tot_all);
+    int row_ex = block_excl_scan256((int)rows, sh_scan, &tot_rows_i);
+    const int64_t own_base = sh_tot[0] + own_ex;
+    const int64_t gstart = sh_tot[2] + row_ex;
+    for (int j = 0; j < own; ++j) {
+      const int64_t idx = own_base + j;
+      if (idx < capacity) {
+        int64_t *rec = out + idx * 5;
+        rec[0] = f;
+        rec[1] = (int64_t)j * bsz;
+        rec[2] = min((int64_t)(j + 1) * bsz, rows);
+        rec[3] = gstart + (int64_t)j * bsz;
+        rec[4] = 0;
+      }
+    }
+    (void)all_ex;
+    __syncthreads();
+    if (tid == 0) {
+      sh_tot[0] += tot_own;
+      sh_tot[1] += tot_all;
+      sh_tot[2] += tot_rows_i;
+    }
+    __syncthreads();
+  }
+  const int64_t own_n = sh_tot[0];
+  const int64_t all_n = sh_tot[1];
+  if (tid == 0) {
+    *local_count = own_n;
+    *count = pad_to > own_n ? pad_to : own_n;
+  }
+  if (pad_to <= own_n) return;
+  __syncthreads();
+  if (own_n > 0) {
+    // cycle own records
+    for (int64_t i = own_n + tid; i < pad_to; i += 256) {
+      if (i >= capacity) break;
+      const int64_t srci = (i - own_n) % own_n;
+      if (srci >= capacity) continue;
+      for (int q = 0; q < 4; ++q) out[i * 5 + q] = out[srci * 5 + q];
+      out[i * 5 + 4] = 1;
+    }
+    return;
+  }
+  if (all_n == 0) {
+    if (tid == 0) *count = 0;
+    return;
+  }
+  // rank owns nothing: cycle the global batch list from index `rank`
+  for (int64_t i = tid; i < pad_to; i += 256) {
+    if (i >= capacity) break;
+    int64_t gidx = (rank + i) % all_n;
+    // locate global batch gidx by walking fragments (nfrag small in practice)
+    int64_t acc = 0, rowbase = 0;
+    for (int f = 0; f < nfrag; ++f) {
+      const int64_t rows = frag_rows[f];
+      const int64_t nbf = (rows + bsz - 1) / bsz;
+      if (gidx < acc + nbf) {
+        const int64_t j = gidx - acc;
+        int64_t *rec = out + i * 5;
+        rec[0] = f;
+        rec[1] = j * bsz;
+        rec[2] = min((j + 1) * bsz, rows);
+        rec[3] = rowbase + j * bsz;
+        rec[4] = 1;
+        break;
+      }
+      acc += nbf;
+      rowbase += rows;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers.
+// ---------------------------------------------------------------------------
+hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
+  if (p.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_destuff, dim3(p.n), dim3(256), 0, s, w.data, p.descs, p.segs, w.dstuf,
+                     w.status);
+  return hipGetLastError();
+}
+
+hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s) {
+  if (p.n == 0 || p.max_blocks == 0) return hipSuccess;
+  dim3 grid((unsigned)((p.max_blocks + 31) / 32), (unsigned)p.n);
+  hipLaunchKernelGGL(k_idct, grid, dim3(256), 0, s, p.descs, p.qtabs, w.coef, w.planes, w.status);
+  return hipGetLastError();
+}
+
+static size_t resize_lds_bytes(int ks_h, int ks_v, int row_bytes) {
+  return 3072 + (size_t)4 * (kOut * ks_h + kBandRows * ks_v + 2 * kOut + 2 * kBandRows) +
+         2 * (size_t)row_bytes;
+}
+
+static int round_row_bytes(int w) { return ((w * 3 + 15) / 16) * 16; }
+
+// Allow up to the full 160 KiB of LDS for the resize kernels (wide images).
+static hipError_t resize_lds_attr() {
+  static hipError_t once = [] {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resize<0>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resize<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return e;
+  }();
+  return once;
+}
+
+hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
+                              hipStream_t s) {
+  if (p.n == 0) return hipSuccess;
+  const int nb = kOut / kBandRows;
+  const int groups = (p.n + 7) / 8;
+  const int row_bytes = round_row_bytes(p.max_w);
+  const size_t lds = resize_lds_bytes(p.max_ks_h, p.max_ks_v, row_bytes);
+  if (lds > 64 * 1024) {
+    hipError_t e = resize_lds_attr();
+    if (e != hipSuccess) return e;
+  }
+  RawSrc raw{nullptr, 0, 0, 0};
+  hipLaunchKernelGGL(k_resize<0>, dim3(groups * 8 * nb), dim3(kResizeThreads), lds, s, p.descs,
+                     w.planes, raw, p.lut, p.labels, out, out_labels, w.status, p.n, p.max_ks_h,
+                     p.max_ks_v, row_bytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_resize_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int w,
+                             const float *lut, float *out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const int nb = kOut / kBandRows;
+  const int groups = (n + 7) / 8;
+  const int ks_h = resample_ksize_host(w, kOut), ks_v = resample_ksize_host(h, kOut);
+  const int row_bytes = round_row_bytes(w);
+  const size_t lds = resize_lds_bytes(ks_h, ks_v, row_bytes);
+  if (lds > 64 * 1024) {
+    hipError_t e = resize_lds_attr();
+    if (e != hipSuccess) return e;
+  }
+  RawSrc raw{hwc, cell_stride, h, w};
+  hipLaunchKernelGGL(k_resize<1>, dim3(groups * 8 * nb), dim3(kResizeThreads), lds, s,
+                     (const ImgDesc *)nullptr, (const uint8_t *)nullptr, raw, lut,
+                     (const int64_t *)nullptr, out, (int64_t *)nullptr, (const int32_t *)nullptr, n,
+                     ks_h, ks_v, row_bytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_resample_coeffs(int in_size, int out_size, int ksize, int32_t *bounds,
+                                  int32_t *kk, hipStream_t s) {
+  hipLaunchKernelGGL(k_resample_coeffs, dim3((out_size + 255) / 256), dim3(256), 0, s, in_size,
+                     out_size, ksize, bounds, kk);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_ranges(int64_t num_rows, int64_t bsz, int rank, int world, int64_t *out,
+                               int64_t capacity, int64_t *count, hipStream_t s) {
+  const int64_t nb = bsz > 0 ? (num_rows + bsz - 1) / bsz : 0;
+  const int64_t cnt = rank < nb ? (nb - rank + world - 1) / world : 0;
+  const int64_t threads = cnt > 0 ? cnt : 1;
+  hipLaunchKernelGGL(k_shard_ranges, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                     num_rows, bsz, rank, world, out, capacity, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_fragments(const int64_t *frag_rows, int nfrag, int64_t bsz, int rank,
+                                  int world, int64_t pad_to, int64_t *out, int64_t capacity,
+                                  int64_t *count, int64_t *local_count, hipStream_t s) {
+  hipLaunchKernelGGL(k_shard_fragments, dim3(1), dim3(256), 0, s, frag_rows, nfrag, bsz, rank,
+                     world, pad_to, out, capacity, count, local_count);
+  return hipGetLastError();
+}
+
+} // namespace ldt

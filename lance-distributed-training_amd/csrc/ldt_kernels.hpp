@@ -1,0 +1,51 @@
+// ldt_kernels.hpp — host-callable launchers for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ldt_types.hpp"
+
+namespace ldt {
+
+__host__ __device__ inline int resample_ksize_host(int inSize, int outSize) {
+  int s = (inSize + outSize - 1) / outSize;
+  if (s < 1) s = 1;
+  return s * 2 + 1;
+}
+
+struct DevPlan {
+  const ImgDesc *descs;
+  Segment *segs;
+  const HuffTab *htabs;
+  const uint16_t *qtabs;
+  const float *lut;
+  const int64_t *labels; // may be null
+  int n, nseg;
+  int max_ks_h, max_ks_v, max_w;
+  int64_t max_blocks;
+};
+
+struct DevWork {
+  const uint8_t *data;  // compressed cells
+  uint8_t *dstuf;       // destuffed entropy data
+  int16_t *coef;        // coefficients
+  uint8_t *planes;      // component planes
+  int32_t *status;      // per image
+};
+
+hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s);
+hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s);
+hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s);
+hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
+                              hipStream_t s);
+hipError_t launch_resize_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int w,
+                             const float *lut, float *out, hipStream_t s);
+hipError_t launch_resample_coeffs(int in_size, int out_size, int ksize, int32_t *bounds,
+                                  int32_t *kk, hipStream_t s);
+hipError_t launch_shard_ranges(int64_t num_rows, int64_t bsz, int rank, int world, int64_t *out,
+                               int64_t capacity, int64_t *count, hipStream_t s);
+hipError_t launch_shard_fragments(const int64_t *frag_rows, int nfrag, int64_t bsz, int rank,
+                                  int world, int64_t pad_to, int64_t *out, int64_t capacity,
+                                  int64_t *count, int64_t *local_count, hipStream_t s);
+
+} // namespace ldt

@@ -1,0 +1,177 @@
+"""ctypes binding of libldt.so (include/ldt.h) and the per-device context.
+
+This is the Python side of the C-ABI boundary: the same stub a maintainer of
+the reference would add. It owns no compute: every decode,
+resize and shard computation runs in the gfx950 kernels of libldt.so. If the
+library is missing or cannot be loaded, importing the product raises — there
+is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must load torch's HIP runtime before libldt.so)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libldt.so")
+
+LDT_OK = 0
+LDT_ERR_ARG = -1
+LDT_ERR_HIP = -2
+LDT_ERR_NOMEM = -3
+LDT_ERR_IMAGE = -4
+
+IMG_OK = 0
+IMG_NOT_JPEG = 1
+IMG_UNSUPPORTED = 2
+IMG_CORRUPT = 3
+IMG_TOO_LARGE = 4
+IMG_NULL = 5
+IMG_STATUS_TEXT = {
+    IMG_NOT_JPEG: "cannot identify image file (not a baseline JPEG)",
+    IMG_UNSUPPORTED: "unsupported JPEG (progressive/arithmetic/12-bit/CMYK/multi-scan)",
+    IMG_CORRUPT: "image file is truncated or corrupt",
+    IMG_TOO_LARGE: "image dimensions exceed LDT_MAX_DIM",
+    IMG_NULL: "null image cell",
+}
+
+OPT_SYNC_STATUS = 1
+OPT_HUFF_MODE = 2
+OPT_SUBSEQ_BITS = 3
+OPT_PROFILE = 4
+
+STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
+
+# Every symbol include/ldt.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "ldt_create", "ldt_destroy", "ldt_last_error", "ldt_set_option", "ldt_version",
+    "ldt_decode_batch", "ldt_decode_batch_large", "ldt_decode_batch_resident",
+    "ldt_fetch_status", "ldt_stage_times", "ldt_resize_raw", "ldt_shard_ranges",
+    "ldt_shard_fragments",
+)
+
+
+class LdtError(RuntimeError):
+    """A libldt call failed (argument, HIP runtime or allocation error)."""
+
+
+class ImageDecodeError(ValueError, OSError):
+    """One or more rows could not be decoded.
+
+    Subclasses OSError so code written against the reference (PIL raises
+    UnidentifiedImageError / OSError from Image.open at lance_iterable.py:42)
+    keeps working, and ValueError per SURVEY.md §8b. ``rows`` maps row index ->
+    LDT_IMG_* status."""
+
+    def __init__(self, rows: dict):
+        self.rows = dict(rows)
+        first = sorted(self.rows)[:8]
+        desc = "; ".join(f"row {i}: {IMG_STATUS_TEXT.get(self.rows[i], self.rows[i])}" for i in first)
+        more = "" if len(self.rows) <= 8 else f" (+{len(self.rows) - 8} more)"
+        super().__init__(f"{len(self.rows)} image(s) failed to decode: {desc}{more}")
+
+
+class Norm(ctypes.Structure):
+    _fields_ = [("mean", ctypes.c_float * 3), ("std", ctypes.c_float * 3)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libldt.so and declare its signatures. Raises if it is missing."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise ImportError(
+                f"libldt.so not found at {p}: build it with `make -C lance-distributed-training_amd` "
+                "or __graft_entry__.build(); the HIP path has no CPU fallback")
+        L = ctypes.CDLL(p)
+        vp, i64, i32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_size_t
+        L.ldt_create.argtypes = [i32, sz, i32]
+        L.ldt_create.restype = vp
+        L.ldt_destroy.argtypes = [vp]
+        L.ldt_destroy.restype = None
+        L.ldt_last_error.argtypes = [vp]
+        L.ldt_last_error.restype = ctypes.c_char_p
+        L.ldt_set_option.argtypes = [vp, i32, i64]
+        L.ldt_version.argtypes = []
+        L.ldt_version.restype = ctypes.c_char_p
+        L.ldt_decode_batch.argtypes = [vp, vp, vp, i64, i64, vp, vp, i64, vp, vp, vp, vp, vp]
+        L.ldt_decode_batch_large.argtypes = [vp, vp, vp, i64, i64, vp, vp, i64, vp, vp, vp, vp, vp]
+        L.ldt_decode_batch_resident.argtypes = [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
+        L.ldt_fetch_status.argtypes = [vp, vp, vp, i64]
+        L.ldt_stage_times.argtypes = [vp, vp, vp, i32]
+        L.ldt_resize_raw.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, vp, vp]
+        L.ldt_shard_ranges.argtypes = [vp, i64, i64, i32, i32, vp, i64, vp, vp]
+        L.ldt_shard_fragments.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, i64, vp, vp, vp]
+        L.ldt_debug_resample_coeffs.argtypes = [vp, i32, i32, vp, vp, vp]
+        for name in ("ldt_set_option", "ldt_decode_batch", "ldt_decode_batch_large",
+                     "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_resize_raw", "ldt_stage_times",
+                     "ldt_shard_ranges", "ldt_shard_fragments", "ldt_debug_resample_coeffs"):
+            getattr(L, name).restype = ctypes.c_int
+        _lib = L
+        return L
+
+
+class Context:
+    """One libldt context per (process, device) — ldt.h threading contract."""
+
+    def __init__(self, device: int):
+        self.lib = load_library()
+        self.device = int(device)
+        self.handle = self.lib.ldt_create(self.device, 0, 0)
+        if not self.handle:
+            raise LdtError(f"ldt_create(device={device}) failed (no HIP device?)")
+        self.lock = threading.Lock()
+
+    def check(self, rc: int, what: str) -> None:
+        if rc == LDT_OK:
+            return
+        msg = self.lib.ldt_last_error(self.handle).decode(errors="replace")
+        raise LdtError(f"{what} failed (rc={rc}): {msg}")
+
+    def set_option(self, opt: int, value: int) -> None:
+        self.check(self.lib.ldt_set_option(self.handle, opt, int(value)), "ldt_set_option")
+
+    def stage_times(self, reset: bool = False):
+        """{stage: (total_ms, launches)} from LDT_OPT_PROFILE events."""
+        import numpy as np
+
+        ms = np.zeros(len(STAGES), np.float64)
+        cnt = np.zeros(len(STAGES), np.int64)
+        self.check(self.lib.ldt_stage_times(self.handle, ms.ctypes.data, cnt.ctypes.data, int(reset)),
+                   "ldt_stage_times")
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(STAGES)}
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                self.lib.ldt_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+_contexts: dict = {}
+_ctx_lock = threading.Lock()
+
+
+def get_context(device: int) -> Context:
+    with _ctx_lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = Context(device)
+            _contexts[device] = ctx
+        return ctx
+
+
+def version() -> str:
+    return load_library().ldt_version().decode()

@@ -1,0 +1,282 @@
+"""Drop-in replacements for the reference's batch transforms.
+
+* ``decode_tensor_image(batch, **kwargs)`` — the iterable ``to_tensor_fn``
+  (reference ``lance_iterable.py:38-50``, registered with
+  ``LanceDataset(..., to_tensor_fn=decode_tensor_image)`` at ``:53-59``).
+* ``collate_fn(batch_of_dicts)`` — the map-style ``collate_fn``
+  (reference ``lance_map_style.py:21-44``, passed to ``get_safe_loader`` at
+  ``:60-69``).
+
+Both return ``{"image": float32[N,3,224,224], "label": int64[N]}`` exactly
+like the reference (PIL ``open -> convert("RGB") -> Resize((224,224)) ->
+ToTensor -> stack``), bit-exact, except that the tensors are already on the
+GPU (``cuda:{LOCAL_RANK}``), so the consumer's ``.to(device)``
+(``lance_iterable.py:108-109``) is a no-op. All arithmetic runs in libldt.so's
+gfx950 kernels; Python only hands over Arrow buffer addresses.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+import pyarrow as pa
+import torch
+
+from . import _lib
+from ._lib import ImageDecodeError, Norm
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)  # lance_iterable.py:31 (commented out there)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+_OUT = 224
+
+
+def default_device() -> torch.device:
+    """cuda:{LOCAL_RANK} as the reference training loop picks (lance_iterable.py:83)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("ldt_amd needs a HIP device (MI355X); no CPU fallback exists")
+    return torch.device("cuda", int(os.environ.get("LOCAL_RANK", torch.cuda.current_device())))
+
+
+def _norm_struct(normalize) -> Optional[Norm]:
+    if not normalize:
+        return None
+    if normalize is True:
+        mean, std = IMAGENET_MEAN, IMAGENET_STD
+    else:
+        mean, std = normalize
+    n = Norm()
+    for c in range(3):
+        n.mean[c] = float(mean[c])
+        n.std[c] = float(std[c])
+    return n
+
+
+def _column(batch, name: str):
+    if isinstance(batch, pa.RecordBatch):
+        return batch.column(batch.schema.get_field_index(name))
+    if isinstance(batch, pa.Table):
+        col = batch.column(name)
+        return col.combine_chunks() if col.num_chunks != 1 else col.chunk(0)
+    raise TypeError(f"expected pyarrow.RecordBatch, got {type(batch).__name__}")
+
+
+def _labels_buffer(batch, label_column: str):
+    """(address, offset, keepalive) of an int64 label column, or None."""
+    if label_column is None:
+        return None
+    names = batch.schema.names
+    if label_column not in names:
+        return None
+    lab = _column(batch, label_column)
+    if lab.null_count:
+        raise ValueError(f"null values in label column {label_column!r}")
+    if lab.type != pa.int64():
+        lab = lab.cast(pa.int64())
+    bufs = lab.buffers()
+    return bufs[1].address, lab.offset, lab
+
+
+class _Decoder:
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.ctx = _lib.get_context(device.index)
+
+
+_decoders: dict = {}
+
+
+def _decoder(device) -> _Decoder:
+    dev = torch.device(device) if device is not None else default_device()
+    if dev.type != "cuda":
+        raise ValueError(f"ldt_amd decodes on a HIP device, got {dev}")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    d = _decoders.get(dev.index)
+    if d is None:
+        d = _Decoder(dev)
+        _decoders[dev.index] = d
+    return d
+
+
+def decode_arrow(images: pa.Array, labels=None, *, device=None, normalize=None,
+                 stream: Optional[torch.cuda.Stream] = None):
+    """Decode an Arrow ``binary``/``large_binary`` array of JPEG cells.
+
+    ``labels``: optional (address, offset, keepalive) as from ``_labels_buffer``
+    or an int64 sequence. Returns (image float32[N,3,224,224], label int64[N] or None).
+    """
+    if isinstance(images, pa.ChunkedArray):
+        images = images.combine_chunks()
+    dec = _decoder(device)
+    ctx = dec.ctx
+    n = len(images)
+    out = torch.empty((n, 3, _OUT, _OUT), dtype=torch.float32, device=dec.device)
+    lbl_keep = None
+    if labels is not None and not isinstance(labels, tuple):
+        arr = np.ascontiguousarray(np.asarray(labels, dtype=np.int64))
+        lbl_keep = arr
+        labels = (arr.ctypes.data, 0, arr)
+    out_lbl = torch.empty((n,), dtype=torch.int64, device=dec.device) if labels is not None else None
+    if n == 0:
+        return out, out_lbl
+    t = images.type
+    if t == pa.binary() or t == pa.string():
+        fn = ctx.lib.ldt_decode_batch
+    elif t == pa.large_binary() or t == pa.large_string():
+        fn = ctx.lib.ldt_decode_batch_large
+    else:
+        raise TypeError(f"image column must be binary or large_binary, got {t}")
+    bufs = images.buffers()
+    validity = bufs[0].address if (bufs[0] is not None and images.null_count) else None
+    offsets, data = bufs[1], bufs[2]
+    data_addr = data.address if data is not None else None
+    if data_addr is None:
+        # all-empty cells: give the library a valid pointer
+        lbl_dummy = np.zeros(8, np.uint8)
+        data_addr = lbl_dummy.ctypes.data
+    status = np.zeros(n, np.int32)
+    norm = _norm_struct(normalize)
+    s = stream if stream is not None else torch.cuda.current_stream(dec.device)
+    with ctx.lock:
+        rc = fn(ctx.handle, data_addr, offsets.address, images.offset, n, validity,
+                labels[0] if labels is not None else None,
+                labels[1] if labels is not None else 0,
+                out.data_ptr(), out_lbl.data_ptr() if out_lbl is not None else None,
+                ctypes.byref(norm) if norm is not None else None,
+                s.cuda_stream, status.ctypes.data)
+    del lbl_keep
+    if rc == _lib.LDT_ERR_IMAGE:
+        bad = {int(i): int(status[i]) for i in np.nonzero(status)[0]}
+        raise ImageDecodeError(bad)
+    ctx.check(rc, "ldt_decode_batch")
+    return out, out_lbl
+
+
+def decode_tensor_image(batch, **kwargs):
+    """to_tensor_fn: ``pa.RecordBatch`` -> ``{"image", "label"}`` (lance_iterable.py:38-50).
+
+    Unknown keyword arguments from LanceDataset are accepted and ignored, as
+    the reference's ``**kwargs`` does. Optional keywords of this build:
+    ``image_column`` ("image"), ``label_column`` ("label"), ``device``,
+    ``normalize`` (False; True = ImageNet mean/std, lance_iterable.py:31).
+    """
+    image_column = kwargs.get("image_column", "image")
+    label_column = kwargs.get("label_column", "label")
+    images = _column(batch, image_column)
+    lab = _labels_buffer(batch, label_column)
+    img, lbl = decode_arrow(images, lab, device=kwargs.get("device"),
+                            normalize=kwargs.get("normalize"), stream=kwargs.get("stream"))
+    out = {"image": img}
+    if lbl is not None:
+        out["label"] = lbl
+    return out
+
+
+def collate_fn(batch_of_dicts, *, device=None, normalize=None):
+    """collate_fn: list of ``{"image": bytes, "label": int}`` -> stacked tensors
+    (lance_map_style.py:21-44). The bytes are packed into one Arrow buffer
+    (zero-copy of the Python ``bytes`` objects is impossible; this is the one
+    host copy) and decoded on the GPU."""
+    images = [item["image"] for item in batch_of_dicts]
+    labels = [item["label"] for item in batch_of_dicts]
+    arr = pa.array(images, type=pa.binary())
+    img, lbl = decode_arrow(arr, labels, device=device, normalize=normalize)
+    return {"image": img, "label": lbl}
+
+
+collate_fn._ldt_device_collate = True  # get_safe_loader: decode in the main process
+
+
+def make_collate_fn(device=None, normalize=None):
+    """A collate_fn bound to a device / Normalize setting."""
+    def _fn(batch_of_dicts):
+        return collate_fn(batch_of_dicts, device=device, normalize=normalize)
+    _fn._ldt_device_collate = True
+    return _fn
+
+
+def resize_raw(hwc, height: int, width: int, *, device=None, normalize=True):
+    """Config 5: raw uint8 HWC cells -> Resize(224,224) [+Normalize] -> float32[N,3,224,224].
+
+    ``hwc`` is a uint8 torch tensor [N, H, W, 3] (host or device) or an Arrow
+    ``binary`` / ``fixed_size_binary(H*W*3)`` array of cells."""
+    dec = _decoder(device)
+    ctx = dec.ctx
+    keep = None
+    if isinstance(hwc, torch.Tensor):
+        if hwc.dtype != torch.uint8 or hwc.dim() != 4 or tuple(hwc.shape[1:]) != (height, width, 3):
+            raise ValueError("expected uint8 [N, H, W, 3]")
+        t = hwc.contiguous()
+        keep = t
+        n = t.shape[0]
+        ptr, is_dev, stride = t.data_ptr(), 1 if t.is_cuda else 0, height * width * 3
+    else:
+        arr = hwc.combine_chunks() if isinstance(hwc, pa.ChunkedArray) else hwc
+        n = len(arr)
+        bufs = arr.buffers()
+        cell = height * width * 3
+        if pa.types.is_fixed_size_binary(arr.type):
+            if arr.type.byte_width != cell:
+                raise ValueError("fixed_size_binary width != H*W*3")
+            ptr = bufs[1].address + arr.offset * cell
+        else:
+            offs = np.frombuffer(bufs[1], dtype=np.int64 if pa.types.is_large_binary(arr.type) else np.int32,
+                                 count=len(arr) + 1 + arr.offset)[arr.offset:]
+            if np.any(np.diff(offs) != cell):
+                raise ValueError("every raw cell must be H*W*3 bytes")
+            ptr = bufs[2].address + int(offs[0])
+        is_dev, stride = 0, cell
+        keep = arr
+    out = torch.empty((n, 3, _OUT, _OUT), dtype=torch.float32, device=dec.device)
+    if n == 0:
+        return out
+    norm = _norm_struct(normalize)
+    s = torch.cuda.current_stream(dec.device)
+    with ctx.lock:
+        rc = ctx.lib.ldt_resize_raw(ctx.handle, ptr, is_dev, n, height, width, stride,
+                                    out.data_ptr(), ctypes.byref(norm) if norm is not None else None,
+                                    s.cuda_stream)
+    ctx.check(rc, "ldt_resize_raw")
+    del keep
+    return out
+
+
+class ResidentBatch:
+    """A batch of JPEG cells staged once into HBM (bench / pre-staged loaders).
+
+    ``decode()`` runs the full decode path with the compressed bytes already
+    resident, so a timed loop measures the GPU path, not PCIe."""
+
+    def __init__(self, cells: Sequence[bytes], labels: Iterable[int] | None = None, *, device=None):
+        dec = _decoder(device)
+        self.dec = dec
+        self.n = len(cells)
+        lens = np.fromiter((len(c) for c in cells), dtype=np.int64, count=self.n)
+        self.offsets = np.zeros(self.n + 1, np.int64)
+        np.cumsum(lens, out=self.offsets[1:])
+        self.host = np.frombuffer(b"".join(cells), dtype=np.uint8).copy() if self.n else np.zeros(1, np.uint8)
+        self.dev = torch.from_numpy(self.host).to(dec.device)
+        self.labels = None if labels is None else np.ascontiguousarray(np.asarray(list(labels), np.int64))
+        self.bytes = int(self.offsets[-1])
+
+    def decode(self, out=None, out_lbl=None, normalize=None):
+        ctx = self.dec.ctx
+        if out is None:
+            out = torch.empty((self.n, 3, _OUT, _OUT), dtype=torch.float32, device=self.dec.device)
+        if self.labels is not None and out_lbl is None:
+            out_lbl = torch.empty((self.n,), dtype=torch.int64, device=self.dec.device)
+        status = np.zeros(self.n, np.int32)
+        norm = _norm_struct(normalize)
+        s = torch.cuda.current_stream(self.dec.device)
+        rc = ctx.lib.ldt_decode_batch_resident(
+            ctx.handle, self.host.ctypes.data, self.dev.data_ptr(), self.offsets.ctypes.data, self.n,
+            self.labels.ctypes.data if self.labels is not None else None,
+            out.data_ptr(), out_lbl.data_ptr() if out_lbl is not None else None,
+            ctypes.byref(norm) if norm is not None else None, s.cuda_stream, status.ctypes.data)
+        if rc == _lib.LDT_ERR_IMAGE:
+            raise ImageDecodeError({int(i): int(status[i]) for i in np.nonzero(status)[0]})
+        ctx.check(rc, "ldt_decode_batch_resident")
+        return out, out_lbl

@@ -1,0 +1,93 @@
+"""CPU tests of the host-side logic around the kernels: the Arrow dataset
+shim, sampler iteration (with the oracle standing in for the index kernel,
+as the checker), error reporting."""
+import numpy as np
+import pyarrow as pa
+import pytest
+
+from oracle import oracle
+
+
+def _frag_compute(rows, B, r, W, pad_to):
+    recs = oracle.sharded_fragment_batches(rows, B, r, W, pad=False)
+    local = len(recs)
+    if pad_to is not None and pad_to >= 0:
+        full = oracle.sharded_fragment_batches(rows, B, r, W, pad=True)
+        # oracle pads to max-over-ranks; trim/extend semantics identical when pad_to == max
+        assert pad_to >= local
+        recs = full[:pad_to] if len(full) >= pad_to else full
+    return recs, local
+
+
+@pytest.fixture()
+def small_ds(tmp_path):
+    from ldt_amd import write_dataset
+
+    n = 1000
+    tbl = pa.table({"image": pa.array([bytes([i % 251]) * (1 + i % 7) for i in range(n)], pa.binary()),
+                    "label": pa.array(np.arange(n) % 101, pa.int64())})
+    return write_dataset(tbl, str(tmp_path / "ds"), max_rows_per_file=300), n
+
+
+def test_write_dataset_fragments(small_ds):
+    ds, n = small_ds
+    assert [f.count_rows() for f in ds.get_fragments()] == [300, 300, 300, 100]
+    assert ds.count_rows() == n
+    rb = ds.read_range(250, 380)  # spans two fragments
+    assert rb.num_rows == 130 and rb.column(1).to_pylist() == list(np.arange(250, 380) % 101)
+
+
+def test_sharded_batch_sampler_iteration(small_ds):
+    from ldt_amd import ShardedBatchSampler
+
+    ds, n = small_ds
+    seen = []
+    for r in range(3):
+        s = ShardedBatchSampler(r, 3, compute=oracle.sharded_batch_ranges)
+        for rb in s(ds, batch_size=64):
+            seen += rb.column(1).to_pylist()
+    assert sorted(seen) == sorted(list(np.arange(n) % 101))
+
+
+def test_sharded_fragment_sampler_iteration(small_ds):
+    from ldt_amd import ShardedFragmentSampler
+
+    ds, n = small_ds
+    counts = []
+    for r in range(3):
+        s = ShardedFragmentSampler(r, 3, compute=_frag_compute)
+        bs = list(s(ds, batch_size=128))
+        counts.append(len(bs))
+        assert all(b.num_rows <= 128 for b in bs)
+    assert counts == [3 + 1, 3, 3]  # rank 0 owns fragments 0 and 3
+
+
+def test_lance_dataset_iterates_to_tensor_fn(small_ds):
+    from ldt_amd import FullScanSampler, LanceDataset
+
+    ds, n = small_ds
+    calls = []
+    lds = LanceDataset(ds, batch_size=100, sampler=FullScanSampler(),
+                       to_tensor_fn=lambda b, **kw: calls.append(b.num_rows) or b.num_rows)
+    assert sum(lds) == n and calls[:3] == [100, 100, 100]
+
+
+def test_safe_dataset_rows(small_ds, tmp_path):
+    from ldt_amd import SafeLanceDataset, get_safe_loader
+
+    ds, n = small_ds
+    sds = SafeLanceDataset(ds.uri)
+    assert len(sds) == n and sds[5]["label"] == 5
+    got = sds.__getitems__([1, 999])
+    assert [g["label"] for g in got] == [1, 999 % 101]
+    dl = get_safe_loader(sds, batch_size=10, collate_fn=lambda rows: [r["label"] for r in rows])
+    first = next(iter(dl))
+    assert first == list(range(10))
+
+
+def test_image_decode_error_is_oserror_and_valueerror():
+    from ldt_amd import ImageDecodeError
+
+    e = ImageDecodeError({3: 1, 0: 3})
+    assert isinstance(e, OSError) and isinstance(e, ValueError)
+    assert "row 0" in str(e) and "row 3" in str(e)
