@@ -241,7 +241,7 @@ struct ldt_ctx {
   bool sync_status = true;
   int huff_mode = 0;
   int subseq_bits = 1024;
-  DevBuf d_data, d_plan, d_dstuf, d_coef, d_planes, d_raw;
+  DevBuf d_data, d_plan, d_dstuf, d_coef, d_planes, d_raw, d_sub, d_pre;
   static constexpr int kSlots = 2;
   PinBuf h_data[kSlots], h_plan[kSlots];
   hipEvent_t slot_ev[kSlots] = {nullptr, nullptr};
@@ -416,6 +416,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   const int64_t base = (int64_t)offsets[arr_offset];
   const int64_t total_bytes = (int64_t)offsets[arr_offset + n] - base;
   if (total_bytes < 0) return set_err(c, LDT_ERR_ARG, "offsets not monotonic");
+  const uint8_t *cells_host = data_host + base; // cell i at cells_host + (offsets[i] - base)
   std::vector<ImgPlan> P((size_t)n);
   std::vector<ImgDesc> D((size_t)n);
   std::vector<Segment> S;
@@ -426,6 +427,10 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   std::unordered_map<int, int> hid_to_batch;
   std::vector<HuffTab> batch_htabs;
   int64_t dst_total = 0, coef_blocks = 0, plane_total = 0, max_blocks = 0;
+  const bool parallel = c->huff_mode != 1;
+  const int SB = c->subseq_bits;
+  int32_t n_wg = 0;
+  std::vector<int32_t> wg_img;
   int max_w = 1, max_ks_h = 3, max_ks_v = 3;
   bool any_bad = false;
   for (int64_t i = 0; i < n; ++i) {
@@ -441,7 +446,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     } else if (ip.cell_len < 0) {
       ip.status = LDT_IMG_NOT_JPEG;
     } else {
-      ip.status = walk_markers(data_host + ip.cell_off, ip.cell_len, ip.H);
+      ip.status = walk_markers(cells_host + ip.cell_off, ip.cell_len, ip.H);
     }
     Header &H = ip.H;
     if (ip.status == LDT_IMG_OK && (H.width > LDT_MAX_DIM || H.height > LDT_MAX_DIM))
@@ -583,6 +588,15 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     }
     d.src_off = ip.cell_off + H.scan_pos;
     d.src_len = ip.cell_len - H.scan_pos;
+    if (parallel) {
+      // subsequence slots: sum over segments of ceil(bits_s / S) <= bits / S + nseg
+      const int64_t slots = (d.src_len * 8 + SB - 1) / SB + d.nseg;
+      d.wg_count = (int32_t)((slots + kSyncThreads - 1) / kSyncThreads);
+      d.wg_first = n_wg;
+      d.sub_cap = d.wg_count * kSyncThreads;
+      for (int q = 0; q < d.wg_count; ++q) wg_img.push_back((int32_t)i);
+      n_wg += d.wg_count;
+    }
     d.dst_off = dst_total;
     dst_total += align_up(d.src_len + 16, 16);
     d.coef_off = coef_blocks;
@@ -617,6 +631,10 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   off = align_up(off + (labels ? 8 * n : 0), 64);
   const int64_t off_status = off;
   off = align_up(off + 4 * n, 64);
+  const int64_t off_wg = off;
+  off = align_up(off + 4 * (int64_t)n_wg, 64);
+  const int64_t off_redo = off;
+  off = align_up(off + 64, 64);
   const int64_t plan_bytes = off;
   ph.has_labels = labels ? 1 : 0;
   ph.max_ks_h = max_ks_h;
@@ -638,18 +656,25 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   build_lut(norm, reinterpret_cast<float *>(hp + ph.off_lut));
   if (labels) memcpy(hp + ph.off_labels, labels + label_offset, 8 * (size_t)n);
   memcpy(hp + off_status, st.data(), 4 * (size_t)n);
+  if (n_wg) memcpy(hp + off_wg, wg_img.data(), 4 * (size_t)n_wg);
+  memset(hp + off_redo, 0, 64);
 
   // ---- device workspace ----
   if ((rc = ensure_dev(c, c->d_plan, (size_t)plan_bytes, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 128 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
+  if (parallel && n_wg) {
+    const size_t slots = (size_t)n_wg * kSyncThreads;
+    if ((rc = ensure_dev(c, c->d_sub, slots * sizeof(SubState), s))) return rc;
+    if ((rc = ensure_dev(c, c->d_pre, slots * 16, s))) return rc;
+  }
   prof_begin(c, LDT_STAGE_H2D, s);
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
     if ((rc = ensure_pin(c, c->h_data[sl], (size_t)total_bytes + 16))) return rc;
     if ((rc = ensure_dev(c, c->d_data, (size_t)total_bytes + 16, s))) return rc;
-    memcpy(c->h_data[sl].p, data_host, (size_t)total_bytes);
+    memcpy(c->h_data[sl].p, cells_host, (size_t)total_bytes);
     HIPCHK(c, hipMemcpyAsync(c->d_data.p, c->h_data[sl].p, (size_t)total_bytes,
                              hipMemcpyHostToDevice, s));
     dev_cells = static_cast<const uint8_t *>(c->d_data.p);
@@ -674,16 +699,23 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.max_ks_v = max_ks_v;
   p.max_w = max_w;
   p.max_blocks = max_blocks;
+  p.subseq_bits = parallel ? SB : 0;
+  p.n_wg = parallel ? n_wg : 0;
+  p.wg_img = reinterpret_cast<const int32_t *>(dp + off_wg);
+  p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
   DevWork w;
   w.data = dev_cells;
   w.dstuf = static_cast<uint8_t *>(c->d_dstuf.p);
   w.coef = static_cast<int16_t *>(c->d_coef.p);
   w.planes = static_cast<uint8_t *>(c->d_planes.p);
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
+  w.sub = static_cast<SubState *>(c->d_sub.p);
+  w.sub_pre = static_cast<int32_t *>(c->d_pre.p);
 
   HIPCHK(c, launch_destuff(p, w, s));
   prof_mark(c, LDT_STAGE_DESTUFF, s);
-  HIPCHK(c, launch_huff_serial(p, w, s));
+  if (parallel) HIPCHK(c, launch_huff_parallel(p, w, s));
+  else HIPCHK(c, launch_huff_serial(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
   HIPCHK(c, launch_idct(p, w, s));
   prof_mark(c, LDT_STAGE_IDCT, s);
@@ -754,7 +786,8 @@ void ldt_destroy(ldt_ctx *c) {
   if (!c) return;
   DeviceGuard g(c->device);
   (void)hipDeviceSynchronize();
-  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_planes, &c->d_raw};
+  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_planes, &c->d_raw,
+                    &c->d_sub, &c->d_pre};
   for (DevBuf *b : dbs)
     if (b->p) (void)hipFree(b->p);
   for (int k = 0; k < ldt_ctx::kSlots; ++k) {

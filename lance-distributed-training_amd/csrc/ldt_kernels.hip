@@ -22,43 +22,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ldt_device.hpp"
 #include "ldt_kernels.hpp"
 
 #pragma clang fp contract(off)
 
 namespace ldt {
-
-// ---------------------------------------------------------------------------
-// Block-wide exclusive scan (256 threads = 4 waves of 64).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int t = __shfl_up(v, d, 64);
-    if (lane >= d) v += t;
-  }
-  return v;
-}
-
-// Returns the exclusive prefix of v over the block; *total = block sum.
-// `scratch` must hold >= 5 ints; contains a __syncthreads.
-__device__ __forceinline__ int block_excl_scan256(int v, int *scratch, int *total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int inc = wave_incl_scan(v);
-  if (lane == 63) scratch[wave] = inc;
-  __syncthreads();
-  int base = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    int s = scratch[w];
-    if (w < wave) base += s;
-    tot += s;
-  }
-  *total = tot;
-  __syncthreads();
-  return base + inc - v;
-}
 
 // ---------------------------------------------------------------------------
 // k_destuff: one 256-thread workgroup per image, 16 bytes per thread per pass.
@@ -67,7 +36,7 @@ __global__ void __launch_bounds__(256) k_destuff(const uint8_t *__restrict__ dat
                                                  const ImgDesc *__restrict__ descs,
                                                  Segment *__restrict__ segs,
                                                  uint8_t *__restrict__ dst,
-                                                 int32_t *__restrict__ status) {
+                                                 int32_t *__restrict__ status, int subseq_bits) {
   const int img = blockIdx.x;
   const ImgDesc &d = descs[img];
   if (status[img] != 0) return;
@@ -159,6 +128,29 @@ __global__ void __launch_bounds__(256) k_destuff(const uint8_t *__restrict__ dat
     if (rst_base != d.nseg - 1) segs[d.seg_base + s].byte_start = d.dst_off;
     segs[d.seg_base + s].byte_end = e;
   }
+  if (subseq_bits <= 0) return;
+  __syncthreads();
+  // subsequence layout for the parallel Huffman decoder: segment s gets
+  // max(1, ceil(bits / S)) threads, numbered from 0 across the image.
+  int base = 0;
+  for (int s0 = 0; s0 < d.nseg; s0 += 256) {
+    const int s = s0 + tid;
+    int cnt = 0;
+    if (s < d.nseg) {
+      const Segment &sg = segs[d.seg_base + s];
+      const int64_t bits = (sg.byte_end - sg.byte_start) * 8;
+      cnt = (int)((bits + subseq_bits - 1) / subseq_bits);
+      if (cnt < 1) cnt = 1;
+    }
+    int tot;
+    const int ex = block_excl_scan256(cnt, sh_scan, &tot);
+    if (s < d.nseg) {
+      segs[d.seg_base + s].sub_first = base + ex;
+      segs[d.seg_base + s].sub_count = cnt;
+    }
+    base += tot;
+  }
+  if (tid == 0 && base > d.sub_cap) status[img] = 3;
 }
 
 // ---------------------------------------------------------------------------
@@ -591,11 +583,9 @@ __global__ void __launch_bounds__(256) k_shard_fragments(const int64_t *frag_row
                                                          int64_t *local_count) {
   __shared__ int sh_scan[8];
   __shared__ long long sh_tot[3]; // own batches, global batches, rows
-  __shared__ long long sh_max_rank;
   const int tid = threadIdx.x;
   if (tid == 0) {
     sh_tot[0] = sh_tot[1] = sh_tot[2] = 0;
-    sh_max_rank = 0;
   }
   __syncthreads();
   // pass 1: own records
@@ -684,7 +674,7 @@ __global__ void __launch_bounds__(256) k_shard_fragments(const int64_t *frag_row
 hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_destuff, dim3(p.n), dim3(256), 0, s, w.data, p.descs, p.segs, w.dstuf,
-                     w.status);
+                     w.status, p.subseq_bits);
   return hipGetLastError();
 }
 

@@ -23,6 +23,11 @@ struct DevPlan {
   int n, nseg;
   int max_ks_h, max_ks_v, max_w;
   int64_t max_blocks;
+  // parallel Huffman decode
+  int subseq_bits;
+  int n_wg;              // total subsequence workgroups
+  const int32_t *wg_img; // workgroup -> image
+  int32_t *redo;         // set when a workgroup-boundary walk did not converge
 };
 
 struct DevWork {
@@ -31,10 +36,13 @@ struct DevWork {
   int16_t *coef;        // coefficients
   uint8_t *planes;      // component planes
   int32_t *status;      // per image
+  SubState *sub;        // per subsequence thread (n_wg * 256)
+  int32_t *sub_pre;     // exclusive prefix of (nblk, dc0, dc1, dc2) per thread (x4)
 };
 
 hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s);
+hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
                               hipStream_t s);

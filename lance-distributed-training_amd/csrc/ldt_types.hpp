@@ -34,6 +34,11 @@ struct ImgDesc {
   int32_t dct[3], act[3];  // Huffman table indices (plan table array)
   uint8_t bcomp[kMaxBlocksPerMcu], bdx[kMaxBlocksPerMcu], bdy[kMaxBlocksPerMcu];
   uint8_t pad_[2];
+  // parallel Huffman decode: this image's subsequence threads occupy
+  // workgroups [wg_first, wg_first + wg_count) (256 threads each)
+  int32_t wg_first, wg_count;
+  int32_t sub_cap;   // thread slots reserved (>= sum of segment sub_count)
+  int32_t pad2_;
 };
 
 // One entropy-coded segment (a restart interval, or the whole scan).
@@ -41,10 +46,22 @@ struct Segment {
   int32_t img;
   int32_t mcu_first;
   int32_t mcu_count;
-  int32_t pad_;
+  int32_t sub_first;  // first subsequence thread (image-local index), set on device
   int64_t byte_start; // destuffed, absolute in the destuff buffer (set on device)
   int64_t byte_end;
+  int32_t sub_count;  // subsequences of S bits, set on device
+  int32_t pad_[3];
 };
+
+// Per-subsequence-thread decode state of the parallel Huffman decoder.
+struct SubState {
+  int32_t exit_p;   // bit position (segment-relative) of the first symbol at/after the range end
+  int32_t exit_bk;  // (b << 8) | k at that symbol
+  int32_t nblk;     // DC symbols decoded inside the range (blocks started)
+  int32_t dc[3];    // sum of DC differences per component inside the range
+};
+
+constexpr int kSyncThreads = 256;
 
 // Device Huffman table (jdhuff.c d_derived_tbl restated for a 9-bit LUT).
 struct HuffTab {

@@ -240,3 +240,32 @@ def test_lance_dataset_end_to_end(tmp_path):
     first = next(iter(loader))
     for k in (0, 49):
         _check(first["image"][k].cpu().numpy(), oracle.jpeg_to_tensor(cells[k]), f"loader[{k}]")
+
+
+@pytest.mark.parametrize("mode,bits", [(1, 1024), (2, 64), (2, 256), (2, 1024), (2, 4096)])
+def test_huffman_decoder_modes(mode, bits, manifest):
+    """Serial-per-segment and parallel self-synchronising decoders (with small
+    subsequences that force many workgroup-boundary walks) agree bit-exactly."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    ctx = _lib.get_context(torch.cuda.current_device())
+    ctx.set_option(_lib.OPT_HUFF_MODE, mode)
+    ctx.set_option(_lib.OPT_SUBSEQ_BITS, bits)
+    try:
+        cells = [read_golden(e["file"]) for e in manifest["images"]]
+        c2, _ = synth.q90_512(6, seed=5)
+        c4, _ = synth.imagenet_like(6, seed=5)
+        cells += c2 + c4
+        out = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+        for k, b in enumerate(cells):
+            _check(out[k], oracle.jpeg_to_tensor(b), f"mode{mode}/S{bits}[{k}]")
+        bad = read_golden("jpeg/bad_truncated.bin")
+        with pytest.raises(ldt_amd.ImageDecodeError) as ei:
+            ldt_amd.decode_tensor_image(_batch([cells[0], bad]))
+        assert ei.value.rows == {1: 3}
+    finally:
+        ctx.set_option(_lib.OPT_HUFF_MODE, 0)
+        ctx.set_option(_lib.OPT_SUBSEQ_BITS, 1024)
