@@ -2,7 +2,8 @@
 
 Stand-in for the reference's input producer (``create_datasets/
 classification.py:13-63``): FOOD101 cannot be downloaded offline, so images
-are seeded smooth fields + Gaussian noise, encoded exactly as the reference
+are seeded smooth fields + Gaussian noise (sigma 6: 22 KiB per FOOD101-shaped
+q75 image, 65 KiB per 512x512 q90 image, matching SURVEY.md §6 probe sizes), encoded exactly as the reference
 encodes them — ``img.save(buffer, format="JPEG")`` (``:27-29``), i.e. Pillow
 defaults: quality 75, 4:2:0, baseline, standard Huffman tables, no restart
 markers — unless a config asks otherwise (q90, restart markers).
@@ -39,7 +40,7 @@ def encode(img: np.ndarray, **save_kwargs) -> bytes:
     return b.getvalue()
 
 
-def food101_like(n: int, seed: int = 0, noise: float = 20.0) -> Tuple[List[bytes], np.ndarray]:
+def food101_like(n: int, seed: int = 0, noise: float = 6.0) -> Tuple[List[bytes], np.ndarray]:
     """Config 1/3: FOOD101-shaped, PIL defaults (q75 4:2:0, no DRI)."""
     cells = []
     for i in range(n):
@@ -48,14 +49,14 @@ def food101_like(n: int, seed: int = 0, noise: float = 20.0) -> Tuple[List[bytes
     return cells, np.arange(n, dtype=np.int64) % 101
 
 
-def q90_512(n: int, seed: int = 0, noise: float = 20.0) -> Tuple[List[bytes], np.ndarray]:
+def q90_512(n: int, seed: int = 0, noise: float = 6.0) -> Tuple[List[bytes], np.ndarray]:
     """Config 2: 512x512 baseline, 4:2:0, quality 90, no DRI."""
     cells = [encode(field(512, 512, seed * 100003 + i, noise), quality=90, subsampling="4:2:0")
              for i in range(n)]
     return cells, np.arange(n, dtype=np.int64) % 101
 
 
-def imagenet_like(n: int, seed: int = 0, noise: float = 20.0) -> Tuple[List[bytes], np.ndarray]:
+def imagenet_like(n: int, seed: int = 0, noise: float = 6.0) -> Tuple[List[bytes], np.ndarray]:
     """Config 4: variable ~500x375 (W in [333,500], H in [250,500]), q90, restart every MCU row."""
     r = np.random.RandomState(seed + 7)
     cells = []
