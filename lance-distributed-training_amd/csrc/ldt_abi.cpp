@@ -265,6 +265,7 @@ struct ldt_ctx {
   double stage_ms[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
   int64_t stage_cnt[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
   EvSet *cur_ev = nullptr;
+  int64_t last_off_redo = -1; // debug counters of the last batch (plan blob offset)
 };
 
 namespace {
@@ -431,7 +432,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   const int SB = c->subseq_bits;
   int32_t n_wg = 0;
   std::vector<int32_t> wg_img;
-  int max_w = 1, max_ks_h = 3, max_ks_v = 3;
+  int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3;
   bool any_bad = false;
   for (int64_t i = 0; i < n; ++i) {
     ImgPlan &ip = P[(size_t)i];
@@ -465,6 +466,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     if (ip.status == LDT_IMG_OK && H.ncomp == 3) {
       // supported upsampling: every component factor divides the max, <= 2
       int bpm = 0;
+      if (H.h[0] != hmax || H.v[0] != vmax) ip.status = LDT_IMG_UNSUPPORTED; // subsampled luma
       for (int k = 0; k < 3; ++k) {
         if (hmax % H.h[k] || vmax % H.v[k]) ip.status = LDT_IMG_UNSUPPORTED;
         bpm += H.h[k] * H.v[k];
@@ -604,6 +606,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     coef_blocks += nblk;
     if (nblk > max_blocks) max_blocks = nblk;
     if (H.width > max_w) max_w = H.width;
+    if (H.height > max_h) max_h = H.height;
     int kh = resample_ksize_host(H.width, kOut), kv = resample_ksize_host(H.height, kOut);
     if (kh > max_ks_h) max_ks_h = kh;
     if (kv > max_ks_v) max_ks_v = kv;
@@ -698,11 +701,13 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.max_ks_h = max_ks_h;
   p.max_ks_v = max_ks_v;
   p.max_w = max_w;
+  p.max_h = max_h;
   p.max_blocks = max_blocks;
   p.subseq_bits = parallel ? SB : 0;
   p.n_wg = parallel ? n_wg : 0;
   p.wg_img = reinterpret_cast<const int32_t *>(dp + off_wg);
   p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
+  c->last_off_redo = off_redo;
   DevWork w;
   w.data = dev_cells;
   w.dstuf = static_cast<uint8_t *>(c->d_dstuf.p);
@@ -719,7 +724,12 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
   HIPCHK(c, launch_idct(p, w, s));
   prof_mark(c, LDT_STAGE_IDCT, s);
-  HIPCHK(c, launch_resize_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s));
+  {
+    hipError_t rerr = hipSuccess;
+    if (!launch_resize2_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr))
+      rerr = launch_resize_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s);
+    HIPCHK(c, rerr);
+  }
   prof_mark(c, LDT_STAGE_RESIZE, s);
   c->cur_ev = nullptr;
 
@@ -924,8 +934,14 @@ int ldt_resize_raw(ldt_ctx *c, const uint8_t *hwc, int hwc_is_device, int64_t n,
   HIPCHK(c, hipEventRecord(c->slot_ev[sl], s));
   c->slot_used[sl] = true;
   prof_begin(c, LDT_STAGE_RESIZE, s);
-  HIPCHK(c, launch_resize_raw(src, cell_stride, (int)n, h, w,
-                              static_cast<const float *>(c->d_plan.p), out_img_dev, s));
+  {
+    hipError_t rerr = hipSuccess;
+    if (!launch_resize2_raw(src, cell_stride, (int)n, h, w, static_cast<const float *>(c->d_plan.p),
+                            out_img_dev, s, &rerr))
+      rerr = launch_resize_raw(src, cell_stride, (int)n, h, w,
+                               static_cast<const float *>(c->d_plan.p), out_img_dev, s);
+    HIPCHK(c, rerr);
+  }
   prof_mark(c, LDT_STAGE_RESIZE, s);
   c->cur_ev = nullptr;
   if ((rc = finish_call(c, s))) return rc;
@@ -959,6 +975,19 @@ int ldt_shard_fragments(ldt_ctx *c, const int64_t *fragment_rows_dev, int nfrag,
   HIPCHK(c, launch_shard_fragments(fragment_rows_dev, nfrag, batch_size, rank, world_size, pad_to,
                                    out_dev, capacity, out_count_dev, out_local_count_dev,
                                    (hipStream_t)stream));
+  return LDT_OK;
+}
+
+// Debug hook: the parallel Huffman decoder's counters of the last batch
+// (redo, workgroups, rounds sum, rounds max, walks, walks converged at the
+// first slot, walk steps, unbounded fallbacks).
+int ldt_debug_counters(ldt_ctx *c, int32_t *out16, void *stream) {
+  if (!c || !out16) return LDT_ERR_ARG;
+  DeviceGuard g(c->device);
+  if (c->last_off_redo < 0) return set_err(c, LDT_ERR_ARG, "no batch yet");
+  HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+  HIPCHK(c, hipMemcpy(out16, static_cast<uint8_t *>(c->d_plan.p) + c->last_off_redo, 64,
+                      hipMemcpyDeviceToHost));
   return LDT_OK;
 }
 

@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
     const int32_t *__restrict__ wg_img, int S, SubState *__restrict__ sub,
-    const int32_t *__restrict__ status) {
+    const int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
   __shared__ HuffTab tabs[6];
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinBytes / 4];
   __shared__ int32_t ex_p[kSyncThreads], ex_bk[kSyncThreads];
@@ -443,7 +443,9 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
     ex_bk[tid] = 0;
   }
   bool need = sc.active && tid > 0 && sc.j > 0;
+  int rounds_done = 0;
   for (int round = 0; round < kSyncThreads + 1; ++round) {
+    ++rounds_done;
     __syncthreads();
     if (tid == 0) any_changed = 0;
     bool changed = false;
@@ -471,6 +473,11 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
     if (!any_changed) break;
     need = sc.active && tid > 0 && sc.j > 0 && chg[tid - 1];
   }
+  if (tid == 0 && dbg) {
+    atomicAdd(dbg + 1, 1);
+    atomicAdd(dbg + 2, rounds_done);
+    atomicMax(dbg + 3, rounds_done);
+  }
   if (sc.active) {
     SubState st;
     st.exit_p = ex_p[tid];
@@ -490,7 +497,7 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
 __device__ void boundary_walk(const ImgDesc &d, const Segment *__restrict__ segs,
                               const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
                               int S, SubState *__restrict__ sub, int64_t gt0, int lt0, bool bounded,
-                              int32_t *redo) {
+                              int32_t *redo, int32_t *dbg) {
   const int si = find_segment(segs, d.seg_base, d.nseg, lt0);
   const Segment &sg = segs[si];
   int j = lt0 - sg.sub_first;
@@ -505,7 +512,9 @@ __device__ void boundary_walk(const ImgDesc &d, const Segment *__restrict__ segs
   int64_t gt = gt0;
   int ep = sub[gt - 1].exit_p, ebk = sub[gt - 1].exit_bk;
   const int64_t wg_end = (gt0 / kSyncThreads + 1) * kSyncThreads;
+  int steps = 0;
   while (true) {
+    ++steps;
     int b = ebk >> 8, k = ebk & 255;
     RunAcc acc{0, 0, 0, 0};
     int64_t cur = 0;
@@ -556,7 +565,14 @@ __device__ void boundary_walk(const ImgDesc &d, const Segment *__restrict__ segs
     st.dc[0] = acc.dc0;
     st.dc[1] = acc.dc1;
     st.dc[2] = acc.dc2;
-    if (np == st.exit_p && nbk == st.exit_bk) break; // converged
+    if (np == st.exit_p && nbk == st.exit_bk) {
+      if (dbg) {
+        atomicAdd(dbg + 4, 1);
+        atomicAdd(dbg + 6, steps);
+        if (steps == 1) atomicAdd(dbg + 5, 1);
+      }
+      break; // converged
+    }
     st.exit_p = np;
     st.exit_bk = nbk;
     ep = np;
@@ -566,6 +582,7 @@ __device__ void boundary_walk(const ImgDesc &d, const Segment *__restrict__ segs
     if (j >= sg.sub_count) break; // end of segment: nothing downstream
     if (bounded && gt >= wg_end) {
       atomicExch(redo, 1);
+      if (dbg) atomicAdd(dbg + 7, 1);
       break;
     }
   }
@@ -588,7 +605,7 @@ __global__ void __launch_bounds__(64) k_huff_fix(const ImgDesc *__restrict__ des
   const int lt0 = (w - d.wg_first) * kSyncThreads;
   const Segment &last = segs[d.seg_base + d.nseg - 1];
   if (lt0 == 0 || lt0 >= last.sub_first + last.sub_count) return;
-  boundary_walk(d, segs, htabs, dstuf, S, sub, (int64_t)w * kSyncThreads, lt0, true, redo);
+  boundary_walk(d, segs, htabs, dstuf, S, sub, (int64_t)w * kSyncThreads, lt0, true, redo, redo);
 }
 
 // Fallback when some walk did not converge inside its workgroup: one lane
@@ -601,7 +618,7 @@ __global__ void __launch_bounds__(64) k_huff_fix_serial(const ImgDesc *__restric
                                                         const int32_t *__restrict__ status,
                                                         const int32_t *__restrict__ redo) {
   const int img = blockIdx.x * blockDim.x + threadIdx.x;
-  if (img >= n || *redo == 0 || status[img] != 0) return;
+  if (img >= n || redo[0] == 0 || status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const Segment &last = segs[d.seg_base + d.nseg - 1];
   const int total = last.sub_first + last.sub_count;
@@ -609,7 +626,7 @@ __global__ void __launch_bounds__(64) k_huff_fix_serial(const ImgDesc *__restric
     const int lt0 = wl * kSyncThreads;
     if (lt0 >= total) break;
     boundary_walk(d, segs, htabs, dstuf, S, sub, (int64_t)(d.wg_first + wl) * kSyncThreads, lt0,
-                  false, nullptr);
+                  false, nullptr, nullptr);
   }
 }
 
@@ -695,7 +712,7 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_wg == 0) return hipSuccess;
   hipLaunchKernelGGL(k_huff_sync, dim3(p.n_wg), dim3(kSyncThreads), 0, s, p.descs, p.segs, p.htabs,
-                     w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.status);
+                     w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.status, p.redo);
   hipLaunchKernelGGL(k_huff_fix, dim3((p.n_wg + 63) / 64), dim3(64), 0, s, p.descs, p.segs, p.htabs,
                      w.dstuf, p.wg_img, p.n_wg, p.subseq_bits, w.sub, w.status, p.redo);
   hipLaunchKernelGGL(k_huff_fix_serial, dim3((p.n + 63) / 64), dim3(64), 0, s, p.descs, p.segs,

@@ -306,46 +306,6 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
   *reinterpret_cast<uint2 *>(dstp) = packed;
 }
 
-// ---------------------------------------------------------------------------
-// Pillow Resample.c precompute_coeffs + normalize_coeffs_8bpc for one output
-// index, BILINEAR (support 1.0), box (0, in). IEEE double, no contraction, so
-// the result equals the x86-64 build of Pillow bit for bit.
-// ---------------------------------------------------------------------------
-__device__ int resample_coeffs_one(int inSize, int outSize, int xx, int ksize, int32_t *k,
-                                   int *xmin_out) {
-#pragma clang fp contract(off)
-  const double scale = (double)inSize / (double)outSize;
-  const double filterscale = scale < 1.0 ? 1.0 : scale;
-  const double support = 1.0 * filterscale;
-  const double center = (xx + 0.5) * scale;
-  const double ss = 1.0 / filterscale;
-  int xmin = (int)(center - support + 0.5);
-  if (xmin < 0) xmin = 0;
-  int xmax = (int)(center + support + 0.5);
-  if (xmax > inSize) xmax = inSize;
-  xmax -= xmin;
-  double ww = 0.0;
-  for (int x = 0; x < xmax; ++x) {
-    double t = ((double)(x + xmin) - center + 0.5) * ss;
-    if (t < 0.0) t = -t;
-    double wv = t < 1.0 ? 1.0 - t : 0.0;
-    ww += wv;
-  }
-  for (int x = 0; x < ksize; ++x) {
-    double wv = 0.0;
-    if (x < xmax) {
-      double t = ((double)(x + xmin) - center + 0.5) * ss;
-      if (t < 0.0) t = -t;
-      wv = t < 1.0 ? 1.0 - t : 0.0;
-      if (ww != 0.0) wv = wv / ww;
-    }
-    const double v = wv * (double)(1 << kPrecisionBits);
-    k[x] = (int32_t)(wv < 0 ? (-0.5 + v) : (0.5 + v));
-  }
-  *xmin_out = xmin;
-  return xmax;
-}
-
 // Test hook: coefficient tables for one (in, out) pair.
 __global__ void k_resample_coeffs(int inSize, int outSize, int ksize, int32_t *bounds,
                                   int32_t *kk) {
@@ -357,54 +317,6 @@ __global__ void k_resample_coeffs(int inSize, int outSize, int ksize, int32_t *b
   bounds[2 * xx + 1] = cnt;
 }
 
-__device__ __forceinline__ uint32_t clip8(int32_t in) {
-  if (in >= (1 << kPrecisionBits << 8)) return 255;
-  if (in <= 0) return 0;
-  return (uint32_t)(in >> kPrecisionBits);
-}
-
-// ---------------------------------------------------------------------------
-// Source-row staging for the resize kernel.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// jdsample.c fancy upsampling value of chroma component c at full-res (x, y).
-__device__ __forceinline__ int chroma_at(const ImgDesc &d, const uint8_t *pl, int c, int x, int y) {
-  const int stride = d.plane_stride[c];
-  const int hf = d.hf[c], vf = d.vf[c];
-  if (hf == 1 && vf == 1) return pl[(int64_t)y * stride + x];
-  const int dw = d.cdw[c], dh = d.cdh[c];
-  if (hf == 2 && vf == 2) {
-    const int cx = x >> 1, cy = y >> 1;
-    if (dw <= 2) return pl[(int64_t)cy * stride + cx];
-    const int ny = (y & 1) ? min(cy + 1, dh - 1) : max(cy - 1, 0);
-    const int nx = (x & 1) ? min(cx + 1, dw - 1) : max(cx - 1, 0);
-    const uint8_t *r0 = pl + (int64_t)cy * stride, *r1 = pl + (int64_t)ny * stride;
-    const int thiscol = r0[cx] * 3 + r1[cx];
-    const int nextcol = r0[nx] * 3 + r1[nx];
-    return (thiscol * 3 + nextcol + 8 - (x & 1)) >> 4;
-  }
-  if (hf == 2 && vf == 1) {
-    const int cx = x >> 1;
-    const uint8_t *r0 = pl + (int64_t)y * stride;
-    if (dw <= 2) return r0[cx];
-    const int nx = (x & 1) ? min(cx + 1, dw - 1) : max(cx - 1, 0);
-    return (r0[cx] * 3 + r0[nx] + 1 + (x & 1)) >> 2;
-  }
-  return pl[(int64_t)(y / vf) * stride + (x / hf)];
-}
-
-// jdcolor.c ycc_rgb_convert with the 16-bit fixed-point tables evaluated inline.
-__device__ __forceinline__ void ycc_to_rgb(int Y, int cb, int cr, uint8_t *o) {
-  const int xcr = cr - 128, xcb = cb - 128;
-  const int cr_r = (91881 * xcr + 32768) >> 16;         // FIX(1.40200)
-  const int cb_b = (116130 * xcb + 32768) >> 16;        // FIX(1.77200)
-  const int g = (-22554 * xcb + 32768 + (-46802) * xcr) >> 16; // FIX(0.34414), FIX(0.71414)
-  o[0] = (uint8_t)clampi(Y + cr_r, 0, 255);
-  o[1] = (uint8_t)clampi(Y + g, 0, 255);
-  o[2] = (uint8_t)clampi(Y + cb_b, 0, 255);
-}
-
 // ---------------------------------------------------------------------------
 // k_resize: fused source (JPEG planes or raw HWC) -> Pillow BILINEAR 224x224
 // -> LUT (ToTensor [+Normalize]) -> fp32 CHW. One workgroup = kBandRows output
@@ -414,11 +326,6 @@ __device__ __forceinline__ void ycc_to_rgb(int Y, int cb, int cr, uint8_t *o) {
 // sum of every needed source row and accumulates the vertical taps in
 // registers, so the uint8 intermediate never leaves the thread.
 // ---------------------------------------------------------------------------
-struct RawSrc {
-  const uint8_t *base;
-  int64_t cell_stride;
-  int h, w;
-};
 
 template <int SRC>
 __global__ void __launch_bounds__(kResizeThreads)

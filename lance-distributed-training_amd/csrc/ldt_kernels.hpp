@@ -13,6 +13,12 @@ __host__ __device__ inline int resample_ksize_host(int inSize, int outSize) {
   return s * 2 + 1;
 }
 
+struct RawSrc {
+  const uint8_t *base;
+  int64_t cell_stride;
+  int h, w;
+};
+
 struct DevPlan {
   const ImgDesc *descs;
   Segment *segs;
@@ -21,7 +27,7 @@ struct DevPlan {
   const float *lut;
   const int64_t *labels; // may be null
   int n, nseg;
-  int max_ks_h, max_ks_v, max_w;
+  int max_ks_h, max_ks_v, max_w, max_h;
   int64_t max_blocks;
   // parallel Huffman decode
   int subseq_bits;
@@ -46,6 +52,12 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
                               hipStream_t s);
+// Banded resize (ldt_resize.hip). Return false when the geometry does not fit
+// LDS (the caller then uses the streaming kernel); *err holds launch errors.
+bool launch_resize2_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
+                         hipStream_t s, hipError_t *err);
+bool launch_resize2_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int wd,
+                        const float *lut, float *out, hipStream_t s, hipError_t *err);
 hipError_t launch_resize_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int w,
                              const float *lut, float *out, hipStream_t s);
 hipError_t launch_resample_coeffs(int in_size, int out_size, int ksize, int32_t *bounds,

@@ -269,3 +269,38 @@ def test_huffman_decoder_modes(mode, bits, manifest):
     finally:
         ctx.set_option(_lib.OPT_HUFF_MODE, 0)
         ctx.set_option(_lib.OPT_SUBSEQ_BITS, 1024)
+
+
+def test_large_image_streaming_fallback_and_too_large():
+    """A 3000x2000 source exceeds the banded kernel's LDS budget and takes the
+    streaming k_resize path; a 9000-wide image exceeds LDT_MAX_DIM."""
+    import ldt_amd
+    from ldt_amd import synth
+
+    big = synth.encode(synth.field(2000, 3000, 77, 6.0), quality=85)
+    small = synth.encode(synth.field(300, 200, 78, 6.0))
+    out = ldt_amd.decode_tensor_image(_batch([big, small]))["image"].cpu().numpy()
+    _check(out[0], oracle.jpeg_to_tensor(big), "3000x2000")
+    _check(out[1], oracle.jpeg_to_tensor(small), "300x200 with a large batch-mate")
+    wide = synth.encode(synth.field(8, 9000, 79, 6.0))
+    with pytest.raises(ldt_amd.ImageDecodeError) as ei:
+        ldt_amd.decode_tensor_image(_batch([small, wide]))
+    assert ei.value.rows == {1: 4}
+
+
+def test_tall_bands_large_batches():
+    """Large batches give tall output bands (>32 rows per workgroup): raw and
+    JPEG paths with 400 small cells vs the oracle."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import synth
+
+    raw = np.random.RandomState(9).randint(0, 256, size=(400, 70, 90, 3), dtype=np.uint8)
+    out = ldt_amd.resize_raw(torch.from_numpy(raw).cuda(), 70, 90, normalize=True).cpu().numpy()
+    for k in (0, 1, 199, 399):
+        _check(out[k], oracle.raw_to_tensor(raw[k], normalize=True), f"raw400[{k}]")
+    cells = [synth.encode(synth.field(48 + (i % 5), 40 + (i % 7), i, 6.0)) for i in range(400)]
+    img = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+    for k in (0, 3, 201, 399):
+        _check(img[k], oracle.jpeg_to_tensor(cells[k]), f"jpeg400[{k}]")
