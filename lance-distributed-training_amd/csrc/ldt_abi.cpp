@@ -172,7 +172,8 @@ int walk_markers(const uint8_t *cell, int64_t len, Header &H) {
   }
 }
 
-// jdhuff.c jpeg_make_d_derived_tbl restated into the device table layout.
+// jdhuff.c jpeg_make_d_derived_tbl restated into the device table layout
+// (canonical code assignment, then the two-level lookup of ldt_types.hpp).
 bool build_huff(const RawHuff &r, bool is_dc, HuffTab &t) {
   memset(&t, 0, sizeof(t));
   int code = 0, k = 0;
@@ -200,14 +201,40 @@ bool build_huff(const RawHuff &r, bool is_dc, HuffTab &t) {
     t.vals[j] = r.syms[j];
     if (is_dc && r.syms[j] > 15) return false;
   }
+  // level 1
   for (int j = 0; j < r.nsym; ++j) {
     if (lens[j] <= kLookBits) {
       const int shift = kLookBits - lens[j];
       const int base = codes[j] << shift;
-      for (int q = 0; q < (1 << shift); ++q)
-        t.lut[base + q] = (uint16_t)((lens[j] << 8) | r.syms[j]);
+      for (int q = 0; q < (1 << shift); ++q) t.l1[base + q] = (uint16_t)((lens[j] << 8) | r.syms[j]);
     }
   }
+  // level 2: one 128-entry chunk per distinct 9-bit prefix of a longer code
+  int prefix_chunk[512];
+  for (int q = 0; q < 512; ++q) prefix_chunk[q] = -1;
+  int nchunks = 0;
+  bool overflow = false;
+  for (int j = 0; j < r.nsym; ++j) {
+    if (lens[j] <= kLookBits) continue;
+    const int pre = codes[j] >> (lens[j] - kLookBits);
+    if (prefix_chunk[pre] < 0) {
+      if (nchunks < kL2Chunks) prefix_chunk[pre] = nchunks++;
+      else overflow = true;
+    }
+  }
+  for (int j = 0; j < r.nsym && !overflow; ++j) {
+    if (lens[j] <= kLookBits) continue;
+    const int pre = codes[j] >> (lens[j] - kLookBits);
+    const int rest = lens[j] - kLookBits; // 1..7 bits after the prefix
+    const int sub = (codes[j] & ((1 << rest) - 1)) << (7 - rest);
+    for (int q = 0; q < (1 << (7 - rest)); ++q)
+      t.l2[prefix_chunk[pre] * 128 + sub + q] = (uint16_t)((lens[j] << 8) | r.syms[j]);
+  }
+  for (int q = 0; q < 512; ++q)
+    if (prefix_chunk[q] >= 0) t.l1[q] = overflow ? 0xFFFF : (uint16_t)(0x8000 | prefix_chunk[q]);
+  if (overflow) // every long-code prefix takes the canonical search
+    for (int j = 0; j < r.nsym; ++j)
+      if (lens[j] > kLookBits) t.l1[codes[j] >> (lens[j] - kLookBits)] = 0xFFFF;
   return true;
 }
 
@@ -432,7 +459,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   const int SB = c->subseq_bits;
   int32_t n_wg = 0;
   std::vector<int32_t> wg_img;
-  int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3;
+  int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3, max_tabs = 1;
   bool any_bad = false;
   for (int64_t i = 0; i < n; ++i) {
     ImgPlan &ip = P[(size_t)i];
@@ -575,6 +602,18 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       d.width = d.height = 1;
       continue;
     }
+    {
+      // distinct tables over the image's (component, DC/AC) contexts
+      int ids[6], nd = 0;
+      for (int x = 0; x < 6; ++x) {
+        const int cc = (x >> 1) < d.ncomp ? (x >> 1) : 0;
+        const int tix = (x & 1) ? d.act[cc] : d.dct[cc];
+        bool seen = false;
+        for (int q = 0; q < nd; ++q) seen = seen || ids[q] == tix;
+        if (!seen) ids[nd++] = tix;
+      }
+      if (nd > max_tabs) max_tabs = nd;
+    }
     plane_total = pl;
     d.restart = H.restart;
     const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
@@ -593,9 +632,9 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     if (parallel) {
       // subsequence slots: sum over segments of ceil(bits_s / S) <= bits / S + nseg
       const int64_t slots = (d.src_len * 8 + SB - 1) / SB + d.nseg;
-      d.wg_count = (int32_t)((slots + kSyncThreads - 1) / kSyncThreads);
+      d.wg_count = (int32_t)((slots + kSlotsPerWg - 1) / kSlotsPerWg);
       d.wg_first = n_wg;
-      d.sub_cap = d.wg_count * kSyncThreads;
+      d.sub_cap = d.wg_count * kSlotsPerWg;
       for (int q = 0; q < d.wg_count; ++q) wg_img.push_back((int32_t)i);
       n_wg += d.wg_count;
     }
@@ -707,6 +746,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.n_wg = parallel ? n_wg : 0;
   p.wg_img = reinterpret_cast<const int32_t *>(dp + off_wg);
   p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
+  p.max_tabs = max_tabs;
   c->last_off_redo = off_redo;
   DevWork w;
   w.data = dev_cells;

@@ -231,6 +231,17 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
   return i < 128 ? (uint32_t)(i + 128) : (i < 512 ? 255u : (i < 896 ? 0u : (uint32_t)(i - 896)));
 }
 
+// One wave handles 8 blocks at a time (lane = row r of block bl), exchanging
+// columns/rows through a wave-private LDS tile: no workgroup barriers. A
+// workgroup (4 waves) covers kIdctBlocksPerWg consecutive blocks of one image.
+constexpr int kIdctBlocksPerWg = 128;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
                                               const uint16_t *__restrict__ qtabs,
                                               const int16_t *__restrict__ coef,
@@ -241,30 +252,30 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const int64_t nblk = (int64_t)d.mcux * d.mcuy * d.bpm;
+  const int64_t b0 = (int64_t)blockIdx.x * kIdctBlocksPerWg;
+  if (b0 >= nblk) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bl = lane >> 3, r = lane & 7;
-  const int64_t blk = (int64_t)blockIdx.x * 32 + wave * 8 + bl;
-  if ((int64_t)blockIdx.x * 32 >= nblk) return;
-  const bool valid = blk < nblk;
   int32_t *w = &ws[wave][bl * 72];
-  int comp = 0;
-  int64_t m = 0;
-  int b = 0;
-  if (valid) {
-    m = blk / d.bpm;
-    b = (int)(blk - m * d.bpm);
-    comp = d.bcomp[b];
-    // row r of the block: 8 int16 = 16 bytes, coalesced across the wave
-    const int4 raw = *reinterpret_cast<const int4 *>(coef + (d.coef_off + blk) * 64 + r * 8);
-    const uint4 q4 = *reinterpret_cast<const uint4 *>(qtabs + d.qt[comp] * 64 + r * 8);
-    const int16_t *cv = reinterpret_cast<const int16_t *>(&raw);
-    const uint16_t *qv = reinterpret_cast<const uint16_t *>(&q4);
+  for (int it = 0; it < kIdctBlocksPerWg / 32; ++it) {
+    const int64_t blk = b0 + it * 32 + wave * 8 + bl;
+    const bool valid = blk < nblk;
+    int comp = 0, b = 0;
+    int64_t m = 0;
+    if (valid) {
+      m = blk / d.bpm;
+      b = (int)(blk - m * d.bpm);
+      comp = d.bcomp[b];
+      // row r of the block: 8 int16 = 16 bytes, coalesced across the wave
+      const int4 raw = *reinterpret_cast<const int4 *>(coef + (d.coef_off + blk) * 64 + r * 8);
+      const uint4 q4 = *reinterpret_cast<const uint4 *>(qtabs + d.qt[comp] * 64 + r * 8);
+      const int16_t *cv = reinterpret_cast<const int16_t *>(&raw);
+      const uint16_t *qv = reinterpret_cast<const uint16_t *>(&q4);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) w[r * 8 + j] = (int32_t)cv[j] * (int32_t)qv[j];
-  }
-  __syncthreads();
-  // pass 1: column r of the block (jidctint.c pass 1, with the DC shortcut)
-  if (valid) {
+      for (int j = 0; j < 8; ++j) w[r * 8 + j] = (int32_t)cv[j] * (int32_t)qv[j];
+    }
+    wave_lds_sync();
+    // pass 1: column r of the block (jidctint.c pass 1, with the DC shortcut)
     int32_t x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = w[j * 8 + r];
@@ -277,44 +288,35 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (t.o[j] + (1 << 10)) >> 11; // DESCALE(, 13-2)
     }
+    wave_lds_sync();
 #pragma unroll
     for (int j = 0; j < 8; ++j) w[j * 8 + r] = o[j];
+    wave_lds_sync();
+    // pass 2: row r
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = w[r * 8 + j];
+    uint32_t px[8];
+    if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
+      const uint32_t v = idct_limit((x[0] + (1 << 4)) >> 5); // DESCALE(, PASS1_BITS+3)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) px[j] = v;
+    } else {
+      Islow8 t = islow_1d(x, 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) px[j] = idct_limit((t.o[j] + (1 << 17)) >> 18); // DESCALE(, 13+2+3)
+    }
+    if (valid) {
+      const int mx = (int)(m % d.mcux), my = (int)(m / d.mcux);
+      const int bx = mx * d.ch[comp] + d.bdx[b];
+      const int by = my * d.cv[comp] + d.bdy[b];
+      uint8_t *dstp = planes + d.plane_off[comp] + (int64_t)(by * 8 + r) * d.plane_stride[comp] + bx * 8;
+      uint2 packed;
+      packed.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+      packed.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
+      *reinterpret_cast<uint2 *>(dstp) = packed;
+    }
+    wave_lds_sync(); // the tile is rewritten by the next group
   }
-  __syncthreads();
-  if (!valid) return;
-  // pass 2: row r
-  int32_t x[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = w[r * 8 + j];
-  uint32_t px[8];
-  if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
-    const uint32_t v = idct_limit((x[0] + (1 << 4)) >> 5); // DESCALE(, PASS1_BITS+3)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) px[j] = v;
-  } else {
-    Islow8 t = islow_1d(x, 0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) px[j] = idct_limit((t.o[j] + (1 << 17)) >> 18); // DESCALE(, 13+2+3)
-  }
-  const int mx = (int)(m % d.mcux), my = (int)(m / d.mcux);
-  const int bx = mx * d.ch[comp] + d.bdx[b];
-  const int by = my * d.cv[comp] + d.bdy[b];
-  uint8_t *dstp = planes + d.plane_off[comp] + (int64_t)(by * 8 + r) * d.plane_stride[comp] + bx * 8;
-  uint2 packed;
-  packed.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
-  packed.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
-  *reinterpret_cast<uint2 *>(dstp) = packed;
-}
-
-// Test hook: coefficient tables for one (in, out) pair.
-__global__ void k_resample_coeffs(int inSize, int outSize, int ksize, int32_t *bounds,
-                                  int32_t *kk) {
-  int xx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (xx >= outSize) return;
-  int xmin;
-  int cnt = resample_coeffs_one(inSize, outSize, xx, ksize, kk + (int64_t)xx * ksize, &xmin);
-  bounds[2 * xx] = xmin;
-  bounds[2 * xx + 1] = cnt;
 }
 
 // ---------------------------------------------------------------------------
@@ -587,7 +589,7 @@ hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
 
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n == 0 || p.max_blocks == 0) return hipSuccess;
-  dim3 grid((unsigned)((p.max_blocks + 31) / 32), (unsigned)p.n);
+  dim3 grid((unsigned)((p.max_blocks + kIdctBlocksPerWg - 1) / kIdctBlocksPerWg), (unsigned)p.n);
   hipLaunchKernelGGL(k_idct, grid, dim3(256), 0, s, p.descs, p.qtabs, w.coef, w.planes, w.status);
   return hipGetLastError();
 }

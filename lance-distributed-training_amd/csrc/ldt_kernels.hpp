@@ -34,6 +34,7 @@ struct DevPlan {
   int n_wg;              // total subsequence workgroups
   const int32_t *wg_img; // workgroup -> image
   int32_t *redo;         // set when a workgroup-boundary walk did not converge
+  int max_tabs;          // max distinct Huffman tables of one image (LDS slots)
 };
 
 struct DevWork {

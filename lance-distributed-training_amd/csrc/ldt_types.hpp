@@ -62,11 +62,22 @@ struct SubState {
 };
 
 constexpr int kSyncThreads = 256;
+// Lane 0 of every decode workgroup is a helper that warms up on the previous
+// workgroup's last subsequence; lanes 1..255 own subsequence slots.
+constexpr int kSlotsPerWg = kSyncThreads - 1;
 
-// Device Huffman table (jdhuff.c d_derived_tbl restated for a 9-bit LUT).
+// Device Huffman table: jdhuff.c's d_derived_tbl restated as a two-level
+// lookup. l1 is indexed by the next 9 bits: (code_len << 8) | symbol for codes
+// of <= 9 bits; 0x8000 | chunk for longer codes, whose symbol is l2[chunk]
+// indexed by the following 7 bits; 0xFFFF (tables with more than kL2Chunks
+// long-code prefixes) falls back to the canonical maxcode search. An l2 entry
+// of 0 is an invalid code (libjpeg: warning, 16 bits skipped, value 0).
+constexpr int kL2Chunks = 8;
+constexpr int kTabU16 = 512 + kL2Chunks * 128; // uint16 entries per table in LDS
 struct HuffTab {
-  uint16_t lut[1 << kLookBits]; // (code_len << 8) | symbol; 0 => longer code
-  int32_t maxcode[18];          // [l] largest code of length l (-1 none), [17] sentinel
+  uint16_t l1[512];
+  uint16_t l2[kL2Chunks * 128];
+  int32_t maxcode[18]; // [l] largest code of length l (-1 none), [17] sentinel
   int32_t valoff[18];
   uint8_t vals[256];
 };

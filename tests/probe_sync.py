@@ -4,7 +4,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "lance-distribu
 import torch, ldt_amd
 from ldt_amd import _lib, synth
 ctx = _lib.get_context(0)
-names = ["redo", "wgs", "rounds_sum", "rounds_max", "walks", "walk_first", "walk_steps", "fallbacks"]
+names = ["redo", "wgs", "rounds_sum", "rounds_max", "walks", "walk_first", "walk_steps", "fallbacks", "boundaries"]
 for wl, fn, n in (("c2", synth.q90_512, 64), ("c1", synth.food101_like, 64), ("c4", synth.imagenet_like, 64)):
     cells, labels = fn(n, seed=1)
     for S in (512, 1024, 2048):
@@ -13,4 +13,4 @@ for wl, fn, n in (("c2", synth.q90_512, 64), ("c1", synth.food101_like, 64), ("c
         rb.decode()
         out = np.zeros(16, np.int32)
         ctx.check(ctx.lib.ldt_debug_counters(ctx.handle, out.ctypes.data, None), "dbg")
-        print(wl, S, dict(zip(names, out[:8].tolist())), flush=True)
+        print(wl, S, dict(zip(names, out[:9].tolist())), flush=True)
