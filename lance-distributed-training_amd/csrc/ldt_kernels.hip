@@ -319,6 +319,17 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
   }
 }
 
+// Test hook: coefficient tables for one (in, out) pair.
+__global__ void k_resample_coeffs(int inSize, int outSize, int ksize, int32_t *bounds,
+                                  int32_t *kk) {
+  int xx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (xx >= outSize) return;
+  int xmin;
+  int cnt = resample_coeffs_one(inSize, outSize, xx, ksize, kk + (int64_t)xx * ksize, &xmin);
+  bounds[2 * xx] = xmin;
+  bounds[2 * xx + 1] = cnt;
+}
+
 // ---------------------------------------------------------------------------
 // k_resize: fused source (JPEG planes or raw HWC) -> Pillow BILINEAR 224x224
 // -> LUT (ToTensor [+Normalize]) -> fp32 CHW. One workgroup = kBandRows output
