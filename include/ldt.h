@@ -58,7 +58,8 @@ extern "C" {
                                  later with ldt_fetch_status()                  */
 #define LDT_OPT_HUFF_MODE 2   /* 0 auto (default), 1 serial per segment,
                                  2 parallel self-synchronising subsequences     */
-#define LDT_OPT_SUBSEQ_BITS 3 /* subsequence length for mode 2 (bits)          */
+#define LDT_OPT_SUBSEQ_BITS 3 /* subsequence length for mode 2: 64..2048 bits,
+                                 multiple of 32 (default 1024)                  */
 #define LDT_OPT_PROFILE 4     /* 1: record HIP events around every stage on the
                                  caller's stream (read with ldt_stage_times)    */
 

@@ -201,17 +201,20 @@ bool build_huff(const RawHuff &r, bool is_dc, HuffTab &t) {
     t.vals[j] = r.syms[j];
     if (is_dc && r.syms[j] > 15) return false;
   }
-  // level 1
+  // level 1 (unused codes: the invalid entry)
+  const uint16_t invalid = huff_entry(16, 0, is_dc);
+  for (int q = 0; q < (1 << kLookBits); ++q) t.l1[q] = invalid;
+  for (int q = 0; q < (kL2Chunks << kL2Bits); ++q) t.l2[q] = invalid;
   for (int j = 0; j < r.nsym; ++j) {
     if (lens[j] <= kLookBits) {
       const int shift = kLookBits - lens[j];
       const int base = codes[j] << shift;
-      for (int q = 0; q < (1 << shift); ++q) t.l1[base + q] = (uint16_t)((lens[j] << 8) | r.syms[j]);
+      for (int q = 0; q < (1 << shift); ++q) t.l1[base + q] = huff_entry(lens[j], r.syms[j], is_dc);
     }
   }
-  // level 2: one 128-entry chunk per distinct 9-bit prefix of a longer code
-  int prefix_chunk[512];
-  for (int q = 0; q < 512; ++q) prefix_chunk[q] = -1;
+  // level 2: one chunk per distinct kLookBits-bit prefix of a longer code
+  int prefix_chunk[1 << kLookBits];
+  for (int q = 0; q < (1 << kLookBits); ++q) prefix_chunk[q] = -1;
   int nchunks = 0;
   bool overflow = false;
   for (int j = 0; j < r.nsym; ++j) {
@@ -225,16 +228,16 @@ bool build_huff(const RawHuff &r, bool is_dc, HuffTab &t) {
   for (int j = 0; j < r.nsym && !overflow; ++j) {
     if (lens[j] <= kLookBits) continue;
     const int pre = codes[j] >> (lens[j] - kLookBits);
-    const int rest = lens[j] - kLookBits; // 1..7 bits after the prefix
-    const int sub = (codes[j] & ((1 << rest) - 1)) << (7 - rest);
-    for (int q = 0; q < (1 << (7 - rest)); ++q)
-      t.l2[prefix_chunk[pre] * 128 + sub + q] = (uint16_t)((lens[j] << 8) | r.syms[j]);
+    const int rest = lens[j] - kLookBits; // 1..kL2Bits bits after the prefix
+    const int sub = (codes[j] & ((1 << rest) - 1)) << (kL2Bits - rest);
+    for (int q = 0; q < (1 << (kL2Bits - rest)); ++q)
+      t.l2[(prefix_chunk[pre] << kL2Bits) + sub + q] = huff_entry(lens[j], r.syms[j], is_dc);
   }
-  for (int q = 0; q < 512; ++q)
-    if (prefix_chunk[q] >= 0) t.l1[q] = overflow ? 0xFFFF : (uint16_t)(0x8000 | prefix_chunk[q]);
+  for (int q = 0; q < (1 << kLookBits); ++q)
+    if (prefix_chunk[q] >= 0) t.l1[q] = overflow ? (uint16_t)kHuffCanon : (uint16_t)(prefix_chunk[q] << 5);
   if (overflow) // every long-code prefix takes the canonical search
     for (int j = 0; j < r.nsym; ++j)
-      if (lens[j] > kLookBits) t.l1[codes[j] >> (lens[j] - kLookBits)] = 0xFFFF;
+      if (lens[j] > kLookBits) t.l1[codes[j] >> (lens[j] - kLookBits)] = (uint16_t)kHuffCanon;
   return true;
 }
 
@@ -639,7 +642,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       n_wg += d.wg_count;
     }
     d.dst_off = dst_total;
-    dst_total += align_up(d.src_len + 16, 16);
+    dst_total += align_up(d.src_len + 16 + (int64_t)kSegPad * d.nseg, 16);
     d.coef_off = coef_blocks;
     const int64_t nblk = nmcu * d.bpm;
     coef_blocks += nblk;
@@ -704,12 +707,12 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   // ---- device workspace ----
   if ((rc = ensure_dev(c, c->d_plan, (size_t)plan_bytes, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 64, s))) return rc;
-  if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 128 + 64, s))) return rc;
+  if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 130 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
   if (parallel && n_wg) {
     const size_t slots = (size_t)n_wg * kSyncThreads;
     if ((rc = ensure_dev(c, c->d_sub, slots * sizeof(SubState), s))) return rc;
-    if ((rc = ensure_dev(c, c->d_pre, slots * 16, s))) return rc;
+    if ((rc = ensure_dev(c, c->d_pre, slots * 4, s))) return rc;
   }
   prof_begin(c, LDT_STAGE_H2D, s);
   const uint8_t *dev_cells = data_dev;
@@ -752,6 +755,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.data = dev_cells;
   w.dstuf = static_cast<uint8_t *>(c->d_dstuf.p);
   w.coef = static_cast<int16_t *>(c->d_coef.p);
+  w.dcv = w.coef + coef_blocks * 64;
   w.planes = static_cast<uint8_t *>(c->d_planes.p);
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
   w.sub = static_cast<SubState *>(c->d_sub.p);
@@ -761,6 +765,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   prof_mark(c, LDT_STAGE_DESTUFF, s);
   if (parallel) HIPCHK(c, launch_huff_parallel(p, w, s));
   else HIPCHK(c, launch_huff_serial(p, w, s));
+  HIPCHK(c, launch_dc_scan(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
   HIPCHK(c, launch_idct(p, w, s));
   prof_mark(c, LDT_STAGE_IDCT, s);
@@ -866,7 +871,7 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     c->profile = value != 0;
     return LDT_OK;
   case LDT_OPT_SUBSEQ_BITS:
-    if (value < 64 || value > (1 << 20) || (value & 31))
+    if (value < 64 || value > 2048 || (value & 31))
       return set_err(c, LDT_ERR_ARG, "subsequence bits %lld", (long long)value);
     c->subseq_bits = (int)value;
     return LDT_OK;

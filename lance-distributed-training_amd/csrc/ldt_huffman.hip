@@ -5,12 +5,18 @@
 //   AC: for k = 1..63: rs = HUFF_DECODE(ac_tbl); r = rs >> 4; s = rs & 15;
 //         s != 0: k += r; coef[natural[k]] = HUFF_EXTEND(GET_BITS(s), s)
 //         s == 0: r == 15 ? k += 15 (ZRL) : break (EOB)
-// Bits past a segment's end read as zero (jdhuff.c inserts zeros at a marker).
+// Bits past a segment's end read as zero (jdhuff.c inserts zeros at a marker;
+// here k_destuff leaves kSegPad zero bytes after every segment).
 // Input: destuffed segments (k_destuff). Output: int16 coefficients, natural
 // order, block (mcu, b) at coef_off + mcu * bpm + b (raw, dequantised in k_idct).
 //
-// Two decoders share the symbol step (sym_step):
-//   k_huff_serial    one lane per segment (restart interval or whole scan);
+// The symbol step is uniform for DC and AC: a table entry carries the bits to
+// consume (code + magnitude), the magnitude width s and the advance of the
+// coefficient index k (DC 1, AC r + 1, ZRL 16, EOB 64), so one lookup, one
+// bit-field extract and one add move the state (see ldt_types.hpp).
+//
+// Two decoders share it:
+//   k_huff_serial    one workgroup per image, one lane per segment;
 //   k_huff_sync/fix/scan/write   the self-synchronising parallel decoder
 //                    (Weissenberger & Schmidt, ICPP 2018), see below.
 #include <hip/hip_runtime.h>
@@ -26,7 +32,9 @@ namespace ldt {
 #define LDS_AS __attribute__((address_space(3)))
 typedef const LDS_AS uint32_t *lds_cu32;
 typedef const LDS_AS uint16_t *lds_cu16;
+typedef const LDS_AS uint8_t *lds_cu8;
 typedef LDS_AS uint16_t *lds_u16;
+typedef LDS_AS uint32_t *lds_u32;
 
 __constant__ uint8_t c_natural[80] = {
     0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
@@ -34,168 +42,90 @@ __constant__ uint8_t c_natural[80] = {
     29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
     47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
 
+// Dynamic LDS of every Huffman kernel: [window words][tables] (sync, write) or
+// [tables] (serial, fix). Sizes come from the launcher.
+extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
+
 // ---------------------------------------------------------------------------
-// Bit input: MSB-first over the destuffed bytes of ONE segment, positions are
-// segment-relative 32-bit. Words come from the workgroup's LDS window when
-// inside it, else from global memory; bytes at/after the segment end read 0.
+// Bit input, MSB first. Words are 32-bit big-endian-as-integer: either the
+// workgroup's LDS window (byte-swapped when staged) or global memory. Bit
+// positions are relative to word 0 of the source; a lane adds its pbias to
+// convert segment-relative positions. No bounds checks: every segment is
+// followed by kSegPad zero bytes, and a symbol starting before the segment end
+// reads at most 31 bits from its start.
 // ---------------------------------------------------------------------------
-struct Bits {
-  const uint8_t *g;     // destuffed buffer (global)
-  lds_cu32 win;         // LDS window (wbytes == 0: none)
-  int64_t wbase;        // absolute byte address of win[0] (4-aligned)
-  int32_t wbytes;
-  int64_t seg0;         // absolute byte address of the segment start
-  int32_t endrel;       // segment length in bytes
-  uint64_t buf;         // MSB-aligned
-  int32_t n;            // valid bits in buf
-  int32_t wrel;         // next word to load, bytes relative to seg0 (seg0 + wrel 4-aligned)
-
-  __device__ __forceinline__ uint32_t word(int32_t rel) const {
-    if (rel >= endrel) return 0u;
-    const int64_t a = seg0 + rel;
-    const int64_t o = a - wbase;
-    uint32_t w = (o >= 0 && o + 4 <= wbytes) ? win[o >> 2] : *reinterpret_cast<const uint32_t *>(g + a);
-    w = __builtin_bswap32(w);
-    const int32_t valid = endrel - rel;
-    if (valid < 4) w &= ~(0xFFFFFFFFu >> (8 * valid));
-    return w;
-  }
-  // Position the reader at segment-relative bit `p`.
-  __device__ __forceinline__ void seek(int32_t p) {
-    const int64_t abit = seg0 * 8 + p;
-    const int64_t a = (abit >> 3) & ~(int64_t)3;
-    const int32_t rel = (int32_t)(a - seg0);
-    const int skip = (int)(abit - a * 8);
-    buf = (((uint64_t)word(rel) << 32) | (uint64_t)word(rel + 4)) << skip;
-    n = 64 - skip;
-    wrel = rel + 8;
-  }
-  __device__ __forceinline__ void refill() {
-    if (n <= 32) {
-      buf |= (uint64_t)word(wrel) << (32 - n);
-      n += 32;
-      wrel += 4;
-    }
-  }
-  __device__ __forceinline__ int32_t pos() const { return wrel * 8 - n; }
+struct LdsWords {
+  lds_cu32 w;
+  __device__ __forceinline__ uint32_t operator()(int32_t i) const { return w[i]; }
+};
+struct GlobWords {
+  const uint32_t *w; // 4-aligned
+  __device__ __forceinline__ uint32_t operator()(int32_t i) const { return __builtin_bswap32(w[i]); }
 };
 
-// Table addressing for a context ctx = 2 * component + (AC ? 1 : 0).
-//   LdsTabs: the image's distinct tables copied into LDS (slot per context).
-//   GlobTabs: the plan's tables in global memory.
-// canon() is the global table for the rare canonical-search fallback.
-struct LdsTabs {
-  lds_cu16 base;
-  uint32_t slotmap; // 3 bits per context
-  const HuffTab *g;
+// Reader state: words wi-2 (hi), wi-1 (lo) and wi (nxt, prefetched); o bits
+// of hi are consumed, 1 <= o <= 32, so the next 32 bits are one alignbit.
+template <class W>
+struct Rd {
+  W src;
+  uint32_t hi, lo, nxt;
+  int32_t wi;
+  int32_t o;
+  int32_t p;     // source bit position of the next symbol
+  __device__ __forceinline__ void seek(int32_t q) {
+    const int32_t i = (q - 1) >> 5;
+    hi = i >= 0 ? src(i) : 0u; // q == 0: hi is fully consumed
+    lo = src(i + 1);
+    nxt = src(i + 2);
+    wi = i + 2;
+    o = q - 32 * i;
+    p = q;
+    // settle the seek's loads here: the decode loop's header then inherits no
+    // pending LDS load and waits only on its own lookup (lgkmcnt(0))
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+  __device__ __forceinline__ uint32_t peek() const {
+    return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)(32 - o));
+  }
+  __device__ __forceinline__ void consume(int t) { // t <= 31
+    p += t;
+    o += t;
+    const bool m = o > 32;
+    hi = m ? lo : hi;
+    lo = m ? nxt : lo;
+    o = m ? o - 32 : o;
+    wi += m ? 1 : 0;
+    nxt = src(wi);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Decode constants of one image and the lookup. The state between symbols is
+// (b3, k): 3 * (block within the MCU) and the coefficient index (0: DC next).
+// ---------------------------------------------------------------------------
+struct Dec {
+  lds_cu16 tabs;     // the image's distinct tables, kTabU16 entries per slot
+  uint32_t dcseq;    // LDS table slot of MCU block b's DC table at bits 3b
+  uint32_t acseq;    // ... AC table
+  int b3end;         // 3 * blocks per MCU
+  const HuffTab *g;  // plan tables (canonical fallback)
   const ImgDesc *d;
-  __device__ __forceinline__ lds_cu16 t(int ctx) const {
-    return base + ((slotmap >> (3 * ctx)) & 7) * kTabU16;
-  }
-  __device__ __forceinline__ const HuffTab *canon(int ctx) const {
-    const int c = ctx >> 1, cc = c < d->ncomp ? c : 0;
-    return g + ((ctx & 1) ? d->act[cc] : d->dct[cc]);
-  }
-};
-struct GlobTabs {
-  const HuffTab *g;
-  const ImgDesc *d;
-  __device__ __forceinline__ const HuffTab *canon(int ctx) const {
-    const int c = ctx >> 1, cc = c < d->ncomp ? c : 0;
-    return g + ((ctx & 1) ? d->act[cc] : d->dct[cc]);
-  }
-  __device__ __forceinline__ const uint16_t *t(int ctx) const { return canon(ctx)->l1; }
 };
 
-// jdhuff.c jpeg_huff_decode, two-level lookup (l1 and l2 are contiguous).
-template <class T>
-__device__ __forceinline__ uint32_t huff_lookup(const T &tabs, int ctx, uint32_t w16) {
-  const auto t = tabs.t(ctx);
-  uint32_t e = t[w16 >> 7];
-  if (e & 0x8000) {
-    if (e != 0xFFFF) {
-      e = t[512 + ((e & 0x7F) << 7) + (w16 & 127)];
-    } else {
-      const HuffTab *cn = tabs.canon(ctx);
-      e = 0;
-#pragma unroll
-      for (int l = 16; l > kLookBits; --l)
-        if ((int)(w16 >> (16 - l)) <= cn->maxcode[l])
-          e = ((uint32_t)l << 8) | cn->vals[(cn->valoff[l] + (int)(w16 >> (16 - l))) & 0xFF];
-    }
-  }
-  return e == 0 ? (16u << 8) : e; // invalid code: skip 16 bits, symbol 0
-}
-
-struct RunAcc {
-  int nblk;
-  int dc0, dc1, dc2;
+struct St {
+  int b3, k;
+  __device__ __forceinline__ int bk() const { return (b3 << 8) | k; }
 };
-__device__ __forceinline__ RunAcc acc_add(RunAcc a, RunAcc b) {
-  return RunAcc{a.nblk + b.nblk, a.dc0 + b.dc0, a.dc1 + b.dc1, a.dc2 + b.dc2};
-}
-__device__ __forceinline__ RunAcc acc_sub(RunAcc a, RunAcc b) {
-  return RunAcc{a.nblk - b.nblk, a.dc0 - b.dc0, a.dc1 - b.dc1, a.dc2 - b.dc2};
+
+__device__ __forceinline__ St make_state(int bk) {
+  St st;
+  st.b3 = bk >> 8;
+  st.k = bk & 255;
+  return st;
 }
 
-// Per-image constants: component of block b, 2 bits each; blocks per MCU.
-struct DecConst {
-  uint32_t compmap;
-  int bpm;
-};
-__device__ __forceinline__ DecConst dec_const(const ImgDesc &d) {
-  DecConst dc;
-  dc.compmap = 0;
-  for (int b = 0; b < d.bpm; ++b) dc.compmap |= (uint32_t)(d.bcomp[b] & 3) << (2 * b);
-  dc.bpm = d.bpm;
-  return dc;
-}
-
-// One symbol (DC if k == 0, else AC) and its extra bits; updates (b, k).
-// Returns the coefficient value; zz = zig-zag index written (0 = DC, -1 none),
-// cc = component.
-template <class T>
-__device__ __forceinline__ int sym_step(Bits &B, int &b, int &k, const DecConst &dcn, const T &tabs,
-                                        RunAcc &acc, int &zz, int &cc) {
-  B.refill();
-  const int c = (int)((dcn.compmap >> (2 * b)) & 3);
-  const int ac = k != 0 ? 1 : 0;
-  const uint32_t w16 = (uint32_t)(B.buf >> 48);
-  const uint32_t e = huff_lookup(tabs, 2 * c + ac, w16);
-  const int len = (int)(e >> 8), sym = (int)(e & 0xFF);
-  const int s = ac ? (sym & 15) : sym;
-  const int r = ac ? (sym >> 4) : 0;
-  const uint64_t t = B.buf << len;
-  const uint32_t raw = s ? (uint32_t)(t >> (64 - s)) : 0u;
-  B.buf = t << s;
-  B.n -= len + s;
-  const int v = (s != 0 && (int)raw < (1 << (s - 1))) ? (int)raw - (1 << s) + 1 : (int)raw;
-  cc = c;
-  if (!ac) {
-    acc.nblk += 1;
-    acc.dc0 += c == 0 ? v : 0;
-    acc.dc1 += c == 1 ? v : 0;
-    acc.dc2 += c == 2 ? v : 0;
-    zz = 0;
-    k = 1;
-  } else {
-    if (s) {
-      k += r;
-      zz = k;
-      ++k;
-    } else {
-      zz = -1;
-      k = (r == 15) ? k + 16 : 64;
-    }
-    if (k >= 64) {
-      k = 0;
-      b = (b + 1 == dcn.bpm) ? 0 : b + 1;
-    }
-  }
-  return v;
-}
-
-// Distinct Huffman tables of an image's six contexts, first come first slot.
+// Distinct tables of an image's six contexts (2 * component + AC), first
+// come first slot; slotmap holds 3 bits per context.
 __device__ __forceinline__ int image_slots(const ImgDesc &d, uint32_t &slotmap, int *slot_tab) {
   int ns = 0;
   slotmap = 0;
@@ -215,60 +145,260 @@ __device__ __forceinline__ int image_slots(const ImgDesc &d, uint32_t &slotmap, 
   return ns;
 }
 
-// ---------------------------------------------------------------------------
-// Serial decoder: one lane per segment, tables read from global memory.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ descs,
-                                                    const Segment *__restrict__ segs, int nseg,
-                                                    const HuffTab *__restrict__ htabs,
-                                                    const uint8_t *__restrict__ dstuf,
-                                                    int16_t *__restrict__ coef,
-                                                    int32_t *__restrict__ status) {
-  const int si = blockIdx.x * blockDim.x + threadIdx.x;
-  if (si >= nseg) return;
-  const Segment sg = segs[si];
-  const ImgDesc &d = descs[sg.img];
-  if (status[sg.img] != 0) return;
-  const GlobTabs tabs{htabs, &d};
-  const DecConst dcn = dec_const(d);
-  Bits B;
-  B.g = dstuf;
-  B.win = (lds_cu32)0;
-  B.wbase = 0;
-  B.wbytes = 0;
-  B.seg0 = sg.byte_start;
-  B.endrel = (int32_t)(sg.byte_end - sg.byte_start);
-  B.seek(0);
-  int pred0 = 0, pred1 = 0, pred2 = 0;
-  int b = 0, k = 0;
-  const int64_t total = (int64_t)sg.mcu_count * d.bpm;
-  int64_t cursor = -1;
-  int16_t *coef_seg = coef + (d.coef_off + (int64_t)sg.mcu_first * d.bpm) * 64;
-  RunAcc acc{0, 0, 0, 0};
-  while (true) {
-    if (k == 0) {
+// Copy an image's distinct tables into LDS and return the decode constants.
+__device__ __forceinline__ Dec load_dec(const ImgDesc &d, const HuffTab *__restrict__ htabs,
+                                        lds_u16 tabs, int tid, int nthreads) {
+  int slot_tab[6];
+  uint32_t slotmap;
+  const int ns = image_slots(d, slotmap, slot_tab);
+  constexpr int kWords = kTabU16 / 2;
+  for (int i = tid; i < ns * kWords; i += nthreads) {
+    const int q = i / kWords, o = i - q * kWords;
+    int tix = slot_tab[0];
+#pragma unroll
+    for (int x = 1; x < 6; ++x)
+      if (q == x) tix = slot_tab[x];
+    ((LDS_AS uint32_t *)(tabs + q * kTabU16))[o] = reinterpret_cast<const uint32_t *>(htabs + tix)[o];
+  }
+  Dec dec;
+  dec.tabs = tabs;
+  dec.dcseq = dec.acseq = 0;
+  for (int b = 0; b < d.bpm; ++b) {
+    const int c = d.bcomp[b] & 3;
+    dec.dcseq |= ((slotmap >> (6 * c)) & 7) << (3 * b);
+    dec.acseq |= ((slotmap >> (6 * c + 3)) & 7) << (3 * b);
+  }
+  dec.b3end = 3 * d.bpm;
+  dec.g = htabs;
+  dec.d = &d;
+  return dec;
+}
+
+// Tables with more than kL2Chunks long-code prefixes: jdhuff.c
+// jpeg_huff_decode's canonical search (first length l with code <= maxcode[l]).
+__device__ __attribute__((noinline)) uint32_t lookup_canon(const HuffTab *__restrict__ g,
+                                                           const ImgDesc *__restrict__ d, int b,
+                                                           bool ac, uint32_t pk) {
+  const int c = d->bcomp[b];
+  const HuffTab *cn = g + (ac ? d->act[c] : d->dct[c]);
+  const uint32_t w16 = pk >> 16;
+  for (int l = kLookBits + 1; l <= 16; ++l) {
+    const int code = (int)(w16 >> (16 - l));
+    if (code <= cn->maxcode[l]) return huff_entry(l, cn->vals[(cn->valoff[l] + code) & 0xFF], !ac);
+  }
+  return huff_entry(16, 0, !ac);
+}
+
+// Entry of the symbol whose code starts at the top bit of pk.
+__device__ __forceinline__ uint32_t lookup(const Dec &dec, const St &st, uint32_t pk) {
+  const bool ac = st.k != 0;
+  const uint32_t slot = __builtin_amdgcn_ubfe(ac ? dec.acseq : dec.dcseq, (uint32_t)st.b3, 3u);
+  const lds_cu16 t = dec.tabs + slot * kTabU16;
+  uint32_t e = t[pk >> (32 - kLookBits)];
+  if (__builtin_expect((e & 31) == 0, 0)) {
+    if (e != kHuffCanon)
+      e = t[(1 << kLookBits) + ((e >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
+    else
+      e = lookup_canon(dec.g, dec.d, st.b3 / 3, ac, pk);
+  }
+  return e;
+}
+
+// HUFF_EXTEND of the s magnitude bits following the code.
+__device__ __forceinline__ int ext_value(uint32_t pk, uint32_t e) {
+  const uint32_t total = e & 31, s = (e >> 5) & 15;
+  const int raw = (int)__builtin_amdgcn_ubfe(pk, 32 - total, s);
+  const int half = (1 << s) >> 1;
+  return raw < half ? raw - 2 * half + 1 : raw;
+}
+
+// k += adv; k >= 64 ends the block (EOB advances by 64).
+__device__ __forceinline__ void advance(St &st, const Dec &dec, int adv) {
+  const int k2 = st.k + adv;
+  const bool end = k2 >= 64;
+  int nb = st.b3 + 3;
+  nb = nb == dec.b3end ? 0 : nb;
+  st.b3 = end ? nb : st.b3;
+  st.k = end ? 0 : k2;
+}
+
+// Count-only symbol: blocks started.
+template <class W>
+__device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int &nblk) {
+  const uint32_t pk = R.peek();
+  const uint32_t e = lookup(dec, st, pk);
+  nblk += st.k == 0 ? 1 : 0;
+  R.consume((int)(e & 31));
+  advance(st, dec, (int)(e >> 9));
+}
+
+// Coefficient-writing decode of one range: from the reader's position until
+// it reaches `stop` or the segment's `total` blocks are complete. cursor is
+// the current block (segment-relative, -1 before the first DC). DC symbols
+// store their difference in dcv_seg[cursor] (k_dc_scan adds the predictors).
+template <class W, class NAT>
+__device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
+                                          int64_t &cursor, int64_t total,
+                                          int16_t *__restrict__ coef_seg,
+                                          int16_t *__restrict__ dcv_seg, NAT nat) {
+  while (R.p < stop) {
+    if (st.k == 0) {
       if (cursor + 1 >= total) break;
       ++cursor;
     }
-    int zz, cc;
-    const int v = sym_step(B, b, k, dcn, tabs, acc, zz, cc);
-    if (zz == 0) {
-      const int pv = (cc == 0 ? pred0 : cc == 1 ? pred1 : pred2) + v;
-      pred0 = cc == 0 ? pv : pred0;
-      pred1 = cc == 1 ? pv : pred1;
-      pred2 = cc == 2 ? pv : pred2;
-      coef_seg[cursor * 64] = (int16_t)pv;
-    } else if (zz > 0) {
-      coef_seg[cursor * 64 + c_natural[zz]] = (int16_t)v;
+    const uint32_t pk = R.peek();
+    const uint32_t e = lookup(dec, st, pk);
+    const int v = ext_value(pk, e);
+    const int adv = (int)(e >> 9);
+    if (st.k == 0) {
+      dcv_seg[cursor] = (int16_t)v;
+    } else if ((e >> 5) & 15) {
+      if (cursor >= 0) coef_seg[cursor * 64 + nat[st.k + adv - 1]] = (int16_t)v;
     }
+    R.consume((int)(e & 31));
+    advance(st, dec, adv);
   }
-  if (B.pos() > B.endrel * 8) status[sg.img] = 3; // ran past the data: truncated
+}
+
+// ---------------------------------------------------------------------------
+// Serial decoder: one 64-lane workgroup per image, one lane per segment.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ descs,
+                                                    const Segment *__restrict__ segs,
+                                                    const HuffTab *__restrict__ htabs,
+                                                    const uint8_t *__restrict__ dstuf,
+                                                    int16_t *__restrict__ coef,
+                                                    int16_t *__restrict__ dcv,
+                                                    int32_t *__restrict__ status) {
+  __shared__ uint8_t s_nat[80];
+  const int img = blockIdx.x;
+  if (status[img] != 0) return;
+  const ImgDesc &d = descs[img];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 80; i += 64) s_nat[i] = c_natural[i];
+  const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, tid, 64);
+  __syncthreads();
+  for (int si = d.seg_base + tid; si < d.seg_base + d.nseg; si += 64) {
+    const Segment sg = segs[si];
+    const int32_t seg_bits = (int32_t)((sg.byte_end - sg.byte_start) * 8);
+    Rd<GlobWords> R;
+    R.src.w = reinterpret_cast<const uint32_t *>(dstuf + (sg.byte_start & ~(int64_t)3));
+    const int32_t pbias = (int32_t)(sg.byte_start & 3) * 8;
+    R.seek(pbias);
+    St st = make_state(0);
+    const int64_t total = (int64_t)sg.mcu_count * d.bpm;
+    int64_t cursor = -1;
+    const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
+    // a valid segment ends inside its bits; 64 bits of slack bound a corrupt one
+    write_run(R, st, dec, pbias + seg_bits + 64, cursor, total, coef + blk0 * 64, dcv + blk0,
+              (lds_cu8)s_nat);
+    if (R.p - pbias > seg_bits || cursor + 1 < total || st.k != 0) status[img] = 3; // truncated
+  }
 }
 
 hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s) {
-  if (p.nseg == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_huff_serial, dim3((p.nseg + 63) / 64), dim3(64), 0, s, p.descs, p.segs,
-                     p.nseg, p.htabs, w.dstuf, w.coef, w.status);
+  if (p.n == 0) return hipSuccess;
+  const size_t tab_lds = (size_t)(p.max_tabs < 1 ? 1 : p.max_tabs) * kTabU16 * 2;
+  hipLaunchKernelGGL(k_huff_serial, dim3(p.n), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,
+                     w.dstuf, w.coef, w.dcv, w.status);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// k_dc_scan: DC predictors (jdhuff.c: last_dc_val[ci] += diff, reset to 0 at
+// every restart marker, process_restart). One workgroup per image; thread t
+// owns a run of consecutive blocks; a segmented scan over the threads carries
+// the per-component sums. Stores the absolute DC (JCOEF, truncated) in place.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ descs,
+                                                 int16_t *__restrict__ dcv,
+                                                 const int32_t *__restrict__ status) {
+  __shared__ int s_f[256];
+  __shared__ int s_v[3][256];
+  const int img = blockIdx.x;
+  if (status[img] != 0) return;
+  const ImgDesc &d = descs[img];
+  const int tid = threadIdx.x;
+  const int bpm = d.bpm;
+  const int64_t nblk = (int64_t)d.mcux * d.mcuy * bpm;
+  const int64_t seglen = d.restart ? (int64_t)d.restart * bpm : nblk;
+  uint32_t compmap = 0;
+  for (int b = 0; b < bpm; ++b) compmap |= (uint32_t)(d.bcomp[b] & 3) << (2 * b);
+  const int64_t K = (nblk + 255) / 256;
+  const int64_t lo = (int64_t)tid * K, hi = min(lo + K, nblk);
+  int16_t *v = dcv + d.coef_off;
+  int s0 = 0, s1 = 0, s2 = 0, flag = 0;
+  int b0 = 0;
+  int64_t sp0 = 0;
+  if (lo < hi) {
+    b0 = (int)(lo % bpm);
+    sp0 = lo % seglen;
+  }
+  {
+    int b = b0;
+    int64_t sp = sp0;
+    for (int64_t x = lo; x < hi; ++x) {
+      if (sp == 0) {
+        s0 = s1 = s2 = 0;
+        flag = 1;
+      }
+      const int c = (int)((compmap >> (2 * b)) & 3);
+      const int dv = v[x];
+      s0 += c == 0 ? dv : 0;
+      s1 += c == 1 ? dv : 0;
+      s2 += c == 2 ? dv : 0;
+      b = b + 1 == bpm ? 0 : b + 1;
+      sp = sp + 1 == seglen ? 0 : sp + 1;
+    }
+  }
+  // inclusive segmented scan of (flag, s0, s1, s2) over the threads
+  s_f[tid] = flag;
+  s_v[0][tid] = s0;
+  s_v[1][tid] = s1;
+  s_v[2][tid] = s2;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    int pf = 0, p0 = 0, p1 = 0, p2 = 0;
+    if (tid >= off) {
+      pf = s_f[tid - off];
+      p0 = s_v[0][tid - off];
+      p1 = s_v[1][tid - off];
+      p2 = s_v[2][tid - off];
+    }
+    __syncthreads();
+    if (tid >= off && !flag) {
+      s0 += p0;
+      s1 += p1;
+      s2 += p2;
+      s_v[0][tid] = s0;
+      s_v[1][tid] = s1;
+      s_v[2][tid] = s2;
+    }
+    flag |= pf;
+    s_f[tid] = flag;
+    __syncthreads();
+  }
+  int r0 = tid > 0 ? s_v[0][tid - 1] : 0;
+  int r1 = tid > 0 ? s_v[1][tid - 1] : 0;
+  int r2 = tid > 0 ? s_v[2][tid - 1] : 0;
+  int b = b0;
+  int64_t sp = sp0;
+  for (int64_t x = lo; x < hi; ++x) {
+    if (sp == 0) r0 = r1 = r2 = 0;
+    const int c = (int)((compmap >> (2 * b)) & 3);
+    const int dv = v[x];
+    r0 += c == 0 ? dv : 0;
+    r1 += c == 1 ? dv : 0;
+    r2 += c == 2 ? dv : 0;
+    v[x] = (int16_t)(c == 0 ? r0 : c == 1 ? r1 : r2);
+    b = b + 1 == bpm ? 0 : b + 1;
+    sp = sp + 1 == seglen ? 0 : sp + 1;
+  }
+}
+
+hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
+  if (p.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dc_scan, dim3(p.n), dim3(256), 0, s, p.descs, w.dcv, w.status);
   return hipGetLastError();
 }
 
@@ -285,27 +415,24 @@ hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s)
 // identically from there on — which is why chains started from a guessed
 // state converge (Huffman codes resynchronise).
 //
-// Workgroup w = 256 lanes: lanes 1..255 own slots (w - wg_first)*255 + lane-1;
-// lane 0 is a helper that decodes the subsequence just before lane 1's from a
-// guessed state, giving lane 1 a (usually correct) entry state. Inside the
-// workgroup, lanes re-decode from their predecessor's exit until no exit
-// changes; each lane keeps two checkpoint states of its last trajectory so a
-// re-decode stops as soon as it merges with it. Across workgroups, k_huff_fix
-// compares the helper's candidate with the previous workgroup's last exit and
-// walks (one wave, LDS tables) only on a mismatch.
+// Workgroup w = 256 lanes: lanes kHelpers..255 own slots
+// (w - wg_first) * kSlotsPerWg + lane - kHelpers; lanes 0..kHelpers-1 are
+// helpers that decode the kHelpers subsequences before the first slot, so its
+// entry state is right unless no chain resynchronised within kHelpers * S bits.
+// Inside the workgroup, lanes re-decode from their predecessor's exit until no
+// exit changes; each lane keeps two checkpoint states of its last trajectory
+// so a re-decode stops as soon as it merges with it. Across workgroups,
+// k_huff_fix compares the last helper's exit with the previous workgroup's
+// last exit and walks (one lane, LDS tables) only on a mismatch. The sync pass
+// only counts blocks per range; k_huff_write then decodes every range from its
+// true entry and k_dc_scan adds the DC predictors.
+//
+// LDS window: the workgroup's destuffed bytes, byte-swapped. Without restart
+// markers they span 256 * S/8 + 76 bytes; a workgroup whose ranges span more
+// (many small restart segments, kSegPad apart) reads global memory instead.
 // ===========================================================================
 
-constexpr int kWinBytes = 34 * 1024;
-
-// Copy an image's distinct tables (l1 + l2 = kTabU16 entries each) into LDS.
-__device__ __forceinline__ void load_tabs(const HuffTab *__restrict__ htabs, const int *slot_tab,
-                                          int ns, lds_u16 tabs, int tid, int nthreads) {
-  constexpr int kWords = kTabU16 / 2;
-  for (int i = tid; i < ns * kWords; i += nthreads) {
-    const int q = i / kWords, o = i - q * kWords;
-    ((LDS_AS uint32_t *)(tabs + q * kTabU16))[o] = reinterpret_cast<const uint32_t *>(htabs + slot_tab[q])[o];
-  }
-}
+__host__ __device__ inline int window_bytes(int S) { return 256 * (S / 8) + 512; }
 
 // Locate the segment that owns image-local slot `lt` (sub_first ascending).
 __device__ __forceinline__ int find_segment(const Segment *__restrict__ segs, int seg_base, int nseg,
@@ -321,278 +448,259 @@ __device__ __forceinline__ int find_segment(const Segment *__restrict__ segs, in
 
 // Global state index of image-local slot lt.
 __device__ __forceinline__ int64_t slot_gt(const ImgDesc &d, int lt) {
-  return (int64_t)(d.wg_first + lt / kSlotsPerWg) * kSyncThreads + 1 + lt % kSlotsPerWg;
+  return (int64_t)(d.wg_first + lt / kSlotsPerWg) * kSyncThreads + kHelpers + lt % kSlotsPerWg;
 }
 
 struct SubCtx {
-  int seg;      // segment index (global), -1 if inactive
-  int j;        // subsequence index within the segment (helper: lane 1's j - 1)
+  int seg;        // segment index (global), -1 if idle
+  int j;          // subsequence index within the segment
   int32_t seg_bits;
-  int64_t seg0, seg_end;
-  bool active;  // real slot
-  bool helper;  // lane 0 with something to warm up on
+  int32_t pbias;  // source bit of the segment's bit 0
+  bool active;    // a real slot
+  bool helper;    // a helper lane with a subsequence to decode
+  bool in_lds;    // the workgroup's window is in LDS (else global words)
+  const uint32_t *gw; // global words at the window base
 };
 
-struct WgShared {
-  uint32_t win[kWinBytes / 4];
-  unsigned long long lo, hi;
-};
-
-// Huffman tables: dynamic LDS, (max distinct tables of the batch) x kTabU16.
-extern __shared__ __attribute__((aligned(16))) uint16_t dyn_tabs[];
-#define TABS_LDS ((lds_u16)(dyn_tabs))
-
-// Workgroup setup shared by the sync and write kernels: distinct tables and
-// the workgroup's LDS window of destuffed bytes.
-__device__ __forceinline__ void sub_setup(const ImgDesc &d, const Segment *__restrict__ segs,
-                                          const HuffTab *__restrict__ htabs, int S, WgShared &sh,
-                                          int64_t &wbase, int &wbytes, const uint8_t *dstuf,
-                                          SubCtx &sc, const int *slot_tab, int ns) {
+// Workgroup setup shared by the sync and write kernels: the image's tables
+// and the LDS window.
+__device__ __forceinline__ Dec sub_setup(const ImgDesc &d, const Segment *__restrict__ segs,
+                                         const HuffTab *__restrict__ htabs, int S,
+                                         const uint8_t *__restrict__ dstuf, lds_u32 win,
+                                         lds_u16 tabs, unsigned long long *sh_lohi, SubCtx &sc) {
   const int tid = threadIdx.x;
-  load_tabs(htabs, slot_tab, ns, TABS_LDS, tid, kSyncThreads);
-  const int wl = (int)blockIdx.x - d.wg_first;
+  const Dec dec = load_dec(d, htabs, tabs, tid, kSyncThreads);
+  const int lt0 = ((int)blockIdx.x - d.wg_first) * kSlotsPerWg;
   const Segment &last = segs[d.seg_base + d.nseg - 1];
   const int total_sub = last.sub_first + last.sub_count;
-  const int lt = wl * kSlotsPerWg + (tid == 0 ? 0 : tid - 1);
-  sc.active = tid > 0 && lt < total_sub;
+  sc.active = false;
   sc.helper = false;
   sc.seg = -1;
   sc.j = 0;
   sc.seg_bits = 0;
-  sc.seg0 = sc.seg_end = 0;
+  sc.pbias = 0;
+  int64_t seg0 = 0;
   uint64_t lo = ~0ull, hi = 0;
+  const int lt = tid >= kHelpers ? lt0 + tid - kHelpers : lt0;
   if (lt < total_sub) {
     const int si = find_segment(segs, d.seg_base, d.nseg, lt);
     const Segment &sg = segs[si];
     int j = lt - sg.sub_first;
-    bool use = sc.active;
-    if (tid == 0) {
-      sc.helper = j > 0;
-      use = sc.helper;
-      j -= 1;
+    if (tid >= kHelpers) {
+      sc.active = true;
+    } else {
+      j -= kHelpers - tid;
+      sc.helper = j >= 0;
     }
-    if (use) {
+    if (sc.active || sc.helper) {
       sc.seg = si;
       sc.j = j;
-      sc.seg0 = sg.byte_start;
-      sc.seg_end = sg.byte_end;
+      seg0 = sg.byte_start;
       sc.seg_bits = (int32_t)((sg.byte_end - sg.byte_start) * 8);
       lo = (uint64_t)(sg.byte_start + ((int64_t)j * S) / 8);
       int64_t h = sg.byte_start + ((int64_t)(j + 1) * S) / 8 + 64;
-      if (h > sg.byte_end + 8) h = sg.byte_end + 8;
+      if (h > sg.byte_end + kSegPad) h = sg.byte_end + kSegPad;
       hi = (uint64_t)h;
     }
   }
   if (tid == 0) {
-    sh.lo = ~0ull;
-    sh.hi = 0;
+    sh_lohi[0] = ~0ull;
+    sh_lohi[1] = 0;
   }
   __syncthreads();
   if (hi > 0) {
-    atomicMin(&sh.lo, (unsigned long long)lo);
-    atomicMax(&sh.hi, (unsigned long long)hi);
+    atomicMin(&sh_lohi[0], (unsigned long long)lo);
+    atomicMax(&sh_lohi[1], (unsigned long long)hi);
   }
   __syncthreads();
-  int64_t wb = 0, wl_bytes = 0;
-  if (sh.hi > 0) {
-    wb = (int64_t)sh.lo & ~(int64_t)3;
-    wl_bytes = (((int64_t)sh.hi - wb) + 3) & ~(int64_t)3;
-    if (wl_bytes > kWinBytes) wl_bytes = kWinBytes;
+  int64_t wb = 0, nbytes = 0;
+  if (sh_lohi[1] > 0) {
+    wb = (int64_t)sh_lohi[0] & ~(int64_t)3;
+    nbytes = (((int64_t)sh_lohi[1] - wb) + 3) & ~(int64_t)3;
   }
-  for (int i = tid; i < (int)wl_bytes / 4; i += kSyncThreads)
-    sh.win[i] = *reinterpret_cast<const uint32_t *>(dstuf + wb + 4 * (int64_t)i);
-  wbase = wb;
-  wbytes = (int)wl_bytes;
+  sc.in_lds = nbytes <= window_bytes(S);
+  sc.gw = reinterpret_cast<const uint32_t *>(dstuf + wb);
+  if (sc.in_lds)
+    for (int i = tid; i < (int)nbytes / 4; i += kSyncThreads) win[i] = __builtin_bswap32(sc.gw[i]);
+  sc.pbias = (int32_t)(seg0 - wb) * 8;
   __syncthreads();
-}
-
-__device__ __forceinline__ void bits_init(Bits &B, const uint8_t *dstuf, lds_cu32 win,
-                                          int64_t wbase, int wbytes, int64_t seg0, int64_t seg_end) {
-  B.g = dstuf;
-  B.win = win;
-  B.wbase = wbase;
-  B.wbytes = wbytes;
-  B.seg0 = seg0;
-  B.endrel = (int32_t)(seg_end - seg0);
+  return dec;
 }
 
 // Checkpoints: the state at the first symbol boundary at/after
-// range_start + S/3 and + 2S/3, with the counts accumulated up to it.
+// range_start + S/3 and + 2S/3, with the blocks counted up to it.
 struct Cp {
   int p0, bk0, p1, bk1;
-  RunAcc a0, a1;
+  int a0, a1;
   int n;
 };
 
-// COUNT decode from the reader's position to the first boundary >= stop.
-// COMPARE: stop at the first checkpoint equal to prev's (merge) and adopt
-// prev's tail. Returns true on a merge.
-template <bool COMPARE, class T>
-__device__ __forceinline__ bool count_run(Bits &B, int32_t range_start, int32_t stop, int S, int &b,
-                                          int &k, const DecConst &dcn, const T &tabs, RunAcc &acc,
-                                          Cp &cp, const Cp &prev, const RunAcc &prev_total) {
+template <class W>
+__device__ __forceinline__ void count_until(Rd<W> &R, int32_t lim, St &st, const Dec &dec,
+                                            int &nblk) {
+  while (R.p < lim) count_step(R, st, dec, nblk);
+}
+
+// COUNT decode from the reader's position to the first boundary >= stop
+// (positions in reader coordinates), recording the checkpoints. COMPARE: stop
+// at the first checkpoint equal to prev's (merge) and adopt prev's tail.
+// Returns true on a merge.
+template <bool COMPARE, class W>
+__device__ __forceinline__ bool count_run(Rd<W> &R, int32_t range_start, int32_t stop, int S,
+                                          St &st, const Dec &dec, int &nblk, Cp &cp,
+                                          const Cp &prev, int prev_total) {
   cp.n = 0;
-  int32_t next_cp = range_start + S / 3;
-  while (true) {
-    const int32_t p = B.pos();
-    if (p >= stop) break;
-    if (p >= next_cp) {
-      const int bk = (b << 8) | k;
-      if (cp.n == 0) {
-        if (COMPARE && prev.n > 0 && prev.p0 == p && prev.bk0 == bk) {
-          const RunAcc delta = acc_sub(acc, prev.a0);
-          cp = prev;
-          cp.a0 = acc;
-          cp.a1 = acc_add(prev.a1, delta);
-          acc = acc_add(prev_total, delta);
-          return true;
-        }
-        cp.p0 = p;
-        cp.bk0 = bk;
-        cp.a0 = acc;
-        cp.n = 1;
-        next_cp = range_start + (2 * S) / 3;
-      } else {
-        if (COMPARE && prev.n > 1 && prev.p1 == p && prev.bk1 == bk) {
-          const RunAcc delta = acc_sub(acc, prev.a1);
-          cp.p1 = p;
-          cp.bk1 = bk;
-          cp.a1 = acc;
-          cp.n = 2;
-          acc = acc_add(prev_total, delta);
-          return true;
-        }
-        cp.p1 = p;
-        cp.bk1 = bk;
-        cp.a1 = acc;
-        cp.n = 2;
-        next_cp = 0x7FFFFFFF;
-      }
+  count_until(R, min(range_start + S / 3, stop), st, dec, nblk);
+  if (R.p >= stop) return false;
+  {
+    const int p = R.p, bk = st.bk();
+    if (COMPARE && prev.n > 0 && prev.p0 == p && prev.bk0 == bk) {
+      const int delta = nblk - prev.a0;
+      cp = prev;
+      cp.a0 = nblk;
+      cp.a1 = prev.a1 + delta;
+      nblk = prev_total + delta;
+      return true;
     }
-    int zz, cc;
-    (void)sym_step(B, b, k, dcn, tabs, acc, zz, cc);
+    cp.p0 = p;
+    cp.bk0 = bk;
+    cp.a0 = nblk;
+    cp.n = 1;
   }
+  count_until(R, min(range_start + (2 * S) / 3, stop), st, dec, nblk);
+  if (R.p >= stop) return false;
+  {
+    const int p = R.p, bk = st.bk();
+    if (COMPARE && prev.n > 1 && prev.p1 == p && prev.bk1 == bk) {
+      const int delta = nblk - prev.a1;
+      cp.p1 = p;
+      cp.bk1 = bk;
+      cp.a1 = nblk;
+      cp.n = 2;
+      nblk = prev_total + delta;
+      return true;
+    }
+    cp.p1 = p;
+    cp.bk1 = bk;
+    cp.a1 = nblk;
+    cp.n = 2;
+  }
+  count_until(R, stop, st, dec, nblk);
   return false;
 }
 
-// Phase 1 + intra-workgroup convergence.
-__global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
-    const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
-    const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
-    const int32_t *__restrict__ wg_img, int S, SubState *__restrict__ sub,
-    const int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
-  __shared__ __attribute__((aligned(16))) WgShared sh;
-  __shared__ int32_t ex_p[kSyncThreads], ex_bk[kSyncThreads];
-  __shared__ uint8_t chg[kSyncThreads];
-  __shared__ int any_changed;
-  const int img = wg_img[blockIdx.x];
-  if (status[img] != 0) return;
-  const ImgDesc &d = descs[img];
+struct SyncLds {
+  int32_t ex_p[kSyncThreads], ex_bk[kSyncThreads];
+  uint8_t chg[kSyncThreads];
+  int any_changed;
+};
+
+// Phase 1 + intra-workgroup convergence for one lane; returns its block count.
+template <class W>
+__device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec, int S,
+                                         SyncLds &sh, int32_t *__restrict__ dbg) {
   const int tid = threadIdx.x;
-  int slot_tab[6];
-  uint32_t slotmap;
-  const int ns = image_slots(d, slotmap, slot_tab);
-  const DecConst dcn = dec_const(d);
-  SubCtx sc;
-  int64_t wbase;
-  int wbytes;
-  sub_setup(d, segs, htabs, S, sh, wbase, wbytes, dstuf, sc, slot_tab, ns);
-  const LdsTabs tabs{TABS_LDS, slotmap, htabs, &d};
-  RunAcc acc{0, 0, 0, 0};
+  int nblk = 0;
   Cp cp, none;
   cp.n = 0;
   none.n = 0;
-  int b = 0, k = 0;
-  Bits B;
-  bits_init(B, dstuf, (lds_cu32)sh.win, wbase, wbytes, sc.seg0, sc.seg_end);
-  const int32_t rstart = sc.j * S;
-  const int32_t stop = min((sc.j + 1) * S, sc.seg_bits);
-  // phase 1: every slot (and the helper) decodes its range from a guessed
-  // state (b = 0, k = 0 at the range start); j == 0 starts exactly.
+  St st = make_state(0);
+  Rd<W> R;
+  R.src = src;
+  const int32_t rstart = sc.pbias + sc.j * S;
+  const int32_t stop = sc.pbias + min((sc.j + 1) * S, sc.seg_bits);
+  // phase 1: every slot and helper decodes its range from a guessed state
+  // (b = 0, k = 0 at the range start); j == 0 starts exactly.
   if (sc.active || sc.helper) {
-    B.seek(rstart);
-    count_run<false>(B, rstart, stop, S, b, k, dcn, tabs, acc, cp, none, acc);
-    ex_p[tid] = B.pos();
-    ex_bk[tid] = (b << 8) | k;
+    R.seek(rstart);
+    count_run<false>(R, rstart, stop, S, st, dec, nblk, cp, none, 0);
+    sh.ex_p[tid] = R.p - sc.pbias;
+    sh.ex_bk[tid] = st.bk();
   } else {
-    ex_p[tid] = 0; // helper of a workgroup whose lane 1 starts a segment: exact (0, 0, 0)
-    ex_bk[tid] = 0;
+    sh.ex_p[tid] = 0;
+    sh.ex_bk[tid] = 0;
   }
-  // every slot with an in-workgroup predecessor (lane 1's is the helper) re-decodes
-  bool need = sc.active && sc.j > 0;
+  // every lane with an in-workgroup predecessor in its segment re-decodes
+  bool need = (sc.active || sc.helper) && sc.j > 0 && tid > 0;
   int rounds = 0;
   for (int round = 0; round < kSyncThreads + 1; ++round) {
     ++rounds;
     __syncthreads();
-    if (tid == 0) any_changed = 0;
+    if (tid == 0) sh.any_changed = 0;
     bool changed = false;
     int np = 0, nbk = 0;
     if (need) {
-      const int ep = ex_p[tid - 1], ebk = ex_bk[tid - 1];
-      b = ebk >> 8;
-      k = ebk & 255;
-      const RunAcc prev_total = acc;
+      const int ep = sh.ex_p[tid - 1], ebk = sh.ex_bk[tid - 1];
+      st = make_state(ebk);
+      const int prev_total = nblk;
       const Cp prev = cp;
-      acc = RunAcc{0, 0, 0, 0};
-      B.seek(ep);
-      if (count_run<true>(B, rstart, stop, S, b, k, dcn, tabs, acc, cp, prev, prev_total)) {
-        np = ex_p[tid];
-        nbk = ex_bk[tid];
+      nblk = 0;
+      R.seek(sc.pbias + ep);
+      if (count_run<true>(R, rstart, stop, S, st, dec, nblk, cp, prev, prev_total)) {
+        np = sh.ex_p[tid];
+        nbk = sh.ex_bk[tid];
       } else {
-        np = B.pos();
-        nbk = (b << 8) | k;
+        np = R.p - sc.pbias;
+        nbk = st.bk();
       }
-      changed = (np != ex_p[tid]) || (nbk != ex_bk[tid]);
+      changed = (np != sh.ex_p[tid]) || (nbk != sh.ex_bk[tid]);
     }
     __syncthreads();
-    chg[tid] = changed ? 1 : 0;
+    sh.chg[tid] = changed ? 1 : 0;
     if (changed) {
-      ex_p[tid] = np;
-      ex_bk[tid] = nbk;
-      any_changed = 1;
+      sh.ex_p[tid] = np;
+      sh.ex_bk[tid] = nbk;
+      sh.any_changed = 1;
     }
     __syncthreads();
-    if (!any_changed) break;
-    need = sc.active && sc.j > 0 && chg[tid > 0 ? tid - 1 : 0] && tid > 0;
+    if (!sh.any_changed) break;
+    need = (sc.active || sc.helper) && sc.j > 0 && tid > 0 && sh.chg[tid > 0 ? tid - 1 : 0];
   }
   if (dbg && tid == 0) {
     atomicAdd(dbg + 1, 1);
     atomicAdd(dbg + 2, rounds);
     atomicMax(dbg + 3, rounds);
   }
-  if (sc.active || tid == 0) {
-    SubState st;
-    st.exit_p = ex_p[tid];
-    st.exit_bk = ex_bk[tid];
-    st.nblk = acc.nblk;
-    st.dc[0] = acc.dc0;
-    st.dc[1] = acc.dc1;
-    st.dc[2] = acc.dc2;
-    sub[(int64_t)blockIdx.x * kSyncThreads + tid] = st;
+  return nblk;
+}
+
+__global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
+    const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
+    const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
+    const int32_t *__restrict__ wg_img, int S, SubState *__restrict__ sub,
+    const int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
+  __shared__ SyncLds sh;
+  __shared__ unsigned long long sh_lohi[2];
+  const int img = wg_img[blockIdx.x];
+  if (status[img] != 0) return;
+  const ImgDesc &d = descs[img];
+  const int tid = threadIdx.x;
+  SubCtx sc;
+  const lds_u32 win = (lds_u32)dyn_lds;
+  const Dec dec = sub_setup(d, segs, htabs, S, dstuf, win,
+                            (lds_u16)(dyn_lds + window_bytes(S) / 4), sh_lohi, sc);
+  int nblk;
+  if (sc.in_lds) nblk = sync_lane(LdsWords{(lds_cu32)win}, sc, dec, S, sh, dbg);
+  else nblk = sync_lane(GlobWords{sc.gw}, sc, dec, S, sh, dbg);
+  if (sc.active || tid == kHelpers - 1) {
+    SubState s;
+    s.exit_p = sh.ex_p[tid];
+    s.exit_bk = sh.ex_bk[tid];
+    s.nblk = nblk;
+    s.pad = 0;
+    sub[(int64_t)blockIdx.x * kSyncThreads + tid] = s;
   }
 }
 
-// One wave per workgroup boundary that needs it: load the tables into LDS,
-// then lane 0 walks slots from lt0 (true entry = the stored exit of slot
-// lt0 - 1) until a recomputed exit equals the stored one. bounded = true
-// stops at the end of lt0's workgroup and raises *redo (the next boundary
-// then compared against a stale exit).
-__device__ void boundary_walk_wave(const ImgDesc &d, const Segment *__restrict__ segs,
-                                   const HuffTab *__restrict__ htabs,
-                                   const uint8_t *__restrict__ dstuf, int S,
-                                   SubState *__restrict__ sub, int lt0, bool bounded, int32_t *redo,
-                                   int32_t *dbg) {
-  const int lane = threadIdx.x & 63;
-  int slot_tab[6];
-  uint32_t slotmap;
-  const int ns = image_slots(d, slotmap, slot_tab);
-  load_tabs(htabs, slot_tab, ns, TABS_LDS, lane, 64);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (lane != 0) return;
-  const LdsTabs tabs{TABS_LDS, slotmap, htabs, &d};
-  const DecConst dcn = dec_const(d);
+// Lane 0 of the calling wave walks slots from lt0 (true entry = the stored
+// exit of slot lt0 - 1) until a recomputed exit equals the stored one. The
+// image's tables must already be in LDS (dec). bounded = true stops at the end
+// of lt0's workgroup and raises *redo (the next boundary then compared against
+// a stale exit).
+__device__ void boundary_walk(const ImgDesc &d, const Dec &dec, const Segment *__restrict__ segs,
+                              const uint8_t *__restrict__ dstuf, int S,
+                              SubState *__restrict__ sub, int lt0, bool bounded, int32_t *redo,
+                              int32_t *dbg) {
   const int si = find_segment(segs, d.seg_base, d.nseg, lt0);
   const Segment &sg = segs[si];
   int j = lt0 - sg.sub_first;
@@ -602,26 +710,25 @@ __device__ void boundary_walk_wave(const ImgDesc &d, const Segment *__restrict__
   int ep = pv.exit_p, ebk = pv.exit_bk;
   int lt = lt0;
   const int wg_next = (lt0 / kSlotsPerWg + 1) * kSlotsPerWg;
-  Bits B;
-  bits_init(B, dstuf, (lds_cu32)0, 0, 0, sg.byte_start, sg.byte_end);
+  Rd<GlobWords> R;
+  R.src.w = reinterpret_cast<const uint32_t *>(dstuf + (sg.byte_start & ~(int64_t)3));
+  const int32_t pbias = (int32_t)(sg.byte_start & 3) * 8;
   int steps = 0;
   Cp cp, none;
   none.n = 0;
   while (true) {
     ++steps;
-    int b = ebk >> 8, k = ebk & 255;
-    RunAcc acc{0, 0, 0, 0};
-    B.seek(ep);
-    count_run<false>(B, j * S, min((j + 1) * S, seg_bits), S, b, k, dcn, tabs, acc, cp, none, acc);
-    const int np = B.pos(), nbk = (b << 8) | k;
-    SubState &st = sub[slot_gt(d, lt)];
-    st.nblk = acc.nblk;
-    st.dc[0] = acc.dc0;
-    st.dc[1] = acc.dc1;
-    st.dc[2] = acc.dc2;
-    if (np == st.exit_p && nbk == st.exit_bk) break; // converged
-    st.exit_p = np;
-    st.exit_bk = nbk;
+    St st = make_state(ebk);
+    int nblk = 0;
+    R.seek(pbias + ep);
+    count_run<false>(R, pbias + j * S, pbias + min((j + 1) * S, seg_bits), S, st, dec, nblk, cp,
+                     none, 0);
+    const int np = R.p - pbias, nbk = st.bk();
+    SubState &s = sub[slot_gt(d, lt)];
+    s.nblk = nblk;
+    if (np == s.exit_p && nbk == s.exit_bk) break; // converged
+    s.exit_p = np;
+    s.exit_bk = nbk;
     ep = np;
     ebk = nbk;
     ++lt;
@@ -640,8 +747,9 @@ __device__ void boundary_walk_wave(const ImgDesc &d, const Segment *__restrict__
   }
 }
 
-// One wave per decode workgroup: compare the helper's candidate entry for the
-// workgroup's first slot with the true predecessor exit; walk on a mismatch.
+// One wave per decode workgroup: compare the last helper's candidate entry
+// for the workgroup's first slot with the true predecessor exit; walk on a
+// mismatch.
 __global__ void __launch_bounds__(64) k_huff_fix(const ImgDesc *__restrict__ descs,
                                                  const Segment *__restrict__ segs,
                                                  const HuffTab *__restrict__ htabs,
@@ -659,15 +767,17 @@ __global__ void __launch_bounds__(64) k_huff_fix(const ImgDesc *__restrict__ des
   const Segment &last = segs[d.seg_base + d.nseg - 1];
   if (wl == 0 || lt0 >= last.sub_first + last.sub_count) return;
   const int si = find_segment(segs, d.seg_base, d.nseg, lt0);
-  if (lt0 == segs[si].sub_first) return; // lane 1 starts a segment: exact entry
+  if (lt0 == segs[si].sub_first) return; // the first slot starts a segment: exact entry
   const SubState &pv = sub[slot_gt(d, lt0 - 1)];
-  const SubState &cand = sub[(int64_t)w * kSyncThreads];
+  const SubState &cand = sub[(int64_t)w * kSyncThreads + kHelpers - 1];
   if (threadIdx.x == 0) atomicAdd(redo + 8, 1); // boundaries checked
-  if (pv.exit_p == cand.exit_p && pv.exit_bk == cand.exit_bk) return; // helper was right
-  boundary_walk_wave(d, segs, htabs, dstuf, S, sub, lt0, true, redo, redo);
+  if (pv.exit_p == cand.exit_p && pv.exit_bk == cand.exit_bk) return; // helpers were right
+  const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, threadIdx.x, 64);
+  __syncthreads();
+  if (threadIdx.x == 0) boundary_walk(d, dec, segs, dstuf, S, sub, lt0, true, redo, redo);
 }
 
-// Fallback when a walk did not converge inside its workgroup: one wave per
+// Fallback when a walk did not converge inside its workgroup: one lane per
 // image walks every workgroup boundary in order (always correct).
 __global__ void __launch_bounds__(64) k_huff_fix_serial(const ImgDesc *__restrict__ descs,
                                                         const Segment *__restrict__ segs,
@@ -679,18 +789,19 @@ __global__ void __launch_bounds__(64) k_huff_fix_serial(const ImgDesc *__restric
   const int img = blockIdx.x;
   if (redo[0] == 0 || status[img] != 0) return;
   const ImgDesc &d = descs[img];
+  const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, threadIdx.x, 64);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   const Segment &last = segs[d.seg_base + d.nseg - 1];
   const int total = last.sub_first + last.sub_count;
   for (int wl = 1; wl < d.wg_count; ++wl) {
     const int lt0 = wl * kSlotsPerWg;
     if (lt0 >= total) break;
-    boundary_walk_wave(d, segs, htabs, dstuf, S, sub, lt0, false, nullptr, nullptr);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    __builtin_amdgcn_wave_barrier();
+    boundary_walk(d, dec, segs, dstuf, S, sub, lt0, false, nullptr, nullptr);
   }
 }
 
-// Exclusive prefix of (nblk, dc0, dc1, dc2) over each image's slots.
+// Exclusive prefix of nblk over each image's slots.
 __global__ void __launch_bounds__(256) k_huff_scan(const ImgDesc *__restrict__ descs,
                                                    const Segment *__restrict__ segs,
                                                    const SubState *__restrict__ sub,
@@ -702,101 +813,82 @@ __global__ void __launch_bounds__(256) k_huff_scan(const ImgDesc *__restrict__ d
   const ImgDesc &d = descs[img];
   const Segment &last = segs[d.seg_base + d.nseg - 1];
   const int total = last.sub_first + last.sub_count;
-  int run[4] = {0, 0, 0, 0};
+  int run = 0;
   for (int base = 0; base < total; base += 256) {
     const int lt = base + threadIdx.x;
-    int v[4] = {0, 0, 0, 0};
+    int v = 0;
     int64_t gt = 0;
     if (lt < total) {
       gt = slot_gt(d, lt);
-      const SubState &st = sub[gt];
-      v[0] = st.nblk;
-      v[1] = st.dc[0];
-      v[2] = st.dc[1];
-      v[3] = st.dc[2];
+      v = sub[gt].nblk;
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      int tot;
-      const int ex = block_excl_scan256(v[q], sh_scan, &tot);
-      if (lt < total) pre[gt * 4 + q] = run[q] + ex;
-      run[q] += tot;
-    }
+    int tot;
+    const int ex = block_excl_scan256(v, sh_scan, &tot);
+    if (lt < total) pre[gt] = run + ex;
+    run += tot;
   }
 }
 
+template <class W>
+__device__ __forceinline__ void write_lane(W src, const SubCtx &sc, const Dec &dec, int S,
+                                           const ImgDesc &d, const Segment &sg, int entry, int bk,
+                                           int64_t cursor, int16_t *__restrict__ coef,
+                                           int16_t *__restrict__ dcv, lds_cu8 nat,
+                                           int32_t *__restrict__ status, int img) {
+  St st = make_state(bk);
+  const int64_t total = (int64_t)sg.mcu_count * d.bpm;
+  const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
+  Rd<W> R;
+  R.src = src;
+  R.seek(sc.pbias + entry);
+  write_run(R, st, dec, sc.pbias + min((sc.j + 1) * S, sc.seg_bits), cursor, total,
+            coef + blk0 * 64, dcv + blk0, nat);
+  if (sc.j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
+}
+
 // Final pass: every slot decodes its range from its true entry state and
-// writes coefficients; DC predictors come from the prefix sums.
+// writes coefficients (DC differences to dcv).
 __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
     const int32_t *__restrict__ wg_img, int S, const SubState *__restrict__ sub,
-    const int32_t *__restrict__ pre, int16_t *__restrict__ coef, int32_t *__restrict__ status) {
-  __shared__ __attribute__((aligned(16))) WgShared sh;
+    const int32_t *__restrict__ pre, int16_t *__restrict__ coef, int16_t *__restrict__ dcv,
+    int32_t *__restrict__ status) {
   __shared__ uint8_t s_nat[80];
+  __shared__ unsigned long long sh_lohi[2];
   const int img = wg_img[blockIdx.x];
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
   if (tid < 80) s_nat[tid] = c_natural[tid];
-  int slot_tab[6];
-  uint32_t slotmap;
-  const int ns = image_slots(d, slotmap, slot_tab);
-  const DecConst dcn = dec_const(d);
   SubCtx sc;
-  int64_t wbase;
-  int wbytes;
-  sub_setup(d, segs, htabs, S, sh, wbase, wbytes, dstuf, sc, slot_tab, ns);
+  const lds_u32 win = (lds_u32)dyn_lds;
+  const Dec dec = sub_setup(d, segs, htabs, S, dstuf, win,
+                            (lds_u16)(dyn_lds + window_bytes(S) / 4), sh_lohi, sc);
   if (!sc.active) return;
-  const LDS_AS uint8_t *nat = (const LDS_AS uint8_t *)s_nat;
-  const LdsTabs tabs{TABS_LDS, slotmap, htabs, &d};
   const Segment &sg = segs[sc.seg];
   const int64_t gt = (int64_t)blockIdx.x * kSyncThreads + tid;
-  const int64_t gfirst = slot_gt(d, sg.sub_first);
-  int b = 0, k = 0;
-  int32_t entry = 0;
+  int entry = 0, bk = 0;
   if (sc.j > 0) {
-    const int64_t pg = (tid == 1) ? (int64_t)(blockIdx.x - 1) * kSyncThreads + kSyncThreads - 1 : gt - 1;
+    const int64_t pg = (tid == kHelpers) ? (int64_t)blockIdx.x * kSyncThreads - 1 : gt - 1;
     const SubState &ps = sub[pg];
     entry = ps.exit_p;
-    b = ps.exit_bk >> 8;
-    k = ps.exit_bk & 255;
+    bk = ps.exit_bk;
   }
-  const int32_t *pg4 = pre + gt * 4, *pf4 = pre + gfirst * 4;
-  int pred0 = pg4[1] - pf4[1], pred1 = pg4[2] - pf4[2], pred2 = pg4[3] - pf4[3];
-  int64_t cursor = (int64_t)(pg4[0] - pf4[0]) - 1;
-  const int64_t total = (int64_t)sg.mcu_count * d.bpm;
-  int16_t *coef_seg = coef + (d.coef_off + (int64_t)sg.mcu_first * d.bpm) * 64;
-  const int32_t stop = min((sc.j + 1) * S, sc.seg_bits);
-  Bits B;
-  bits_init(B, dstuf, (lds_cu32)sh.win, wbase, wbytes, sc.seg0, sc.seg_end);
-  B.seek(entry);
-  RunAcc acc{0, 0, 0, 0};
-  while (true) {
-    if (B.pos() >= stop) break;
-    if (k == 0) {
-      if (cursor + 1 >= total) break;
-      ++cursor;
-    }
-    int zz, cc;
-    const int v = sym_step(B, b, k, dcn, tabs, acc, zz, cc);
-    if (zz == 0) {
-      const int pv = (cc == 0 ? pred0 : cc == 1 ? pred1 : pred2) + v;
-      pred0 = cc == 0 ? pv : pred0;
-      pred1 = cc == 1 ? pv : pred1;
-      pred2 = cc == 2 ? pv : pred2;
-      coef_seg[cursor * 64] = (int16_t)pv;
-    } else if (zz > 0 && cursor >= 0) {
-      coef_seg[cursor * 64 + nat[zz]] = (int16_t)v;
-    }
-  }
-  if (sc.j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
+  const int64_t cursor = (int64_t)(pre[gt] - pre[slot_gt(d, sg.sub_first)]) - 1;
+  if (sc.in_lds)
+    write_lane(LdsWords{(lds_cu32)win}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv,
+               (lds_cu8)s_nat, status, img);
+  else
+    write_lane(GlobWords{sc.gw}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv, (lds_cu8)s_nat,
+               status, img);
 }
 
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_wg == 0) return hipSuccess;
   const size_t tab_lds = (size_t)(p.max_tabs < 1 ? 1 : p.max_tabs) * kTabU16 * 2;
-  hipLaunchKernelGGL(k_huff_sync, dim3(p.n_wg), dim3(kSyncThreads), tab_lds, s, p.descs, p.segs,
+  const size_t dec_lds = (size_t)window_bytes(p.subseq_bits) + tab_lds;
+  hipLaunchKernelGGL(k_huff_sync, dim3(p.n_wg), dim3(kSyncThreads), dec_lds, s, p.descs, p.segs,
                      p.htabs, w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.status, p.redo);
   hipLaunchKernelGGL(k_huff_fix, dim3(p.n_wg), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,
                      w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.status, p.redo);
@@ -804,8 +896,9 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
                      w.dstuf, p.subseq_bits, w.sub, w.status, p.redo);
   hipLaunchKernelGGL(k_huff_scan, dim3(p.n), dim3(256), 0, s, p.descs, p.segs, w.sub, w.sub_pre,
                      w.status);
-  hipLaunchKernelGGL(k_huff_write, dim3(p.n_wg), dim3(kSyncThreads), tab_lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.sub_pre, w.coef, w.status);
+  hipLaunchKernelGGL(k_huff_write, dim3(p.n_wg), dim3(kSyncThreads), dec_lds, s, p.descs, p.segs,
+                     p.htabs, w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.sub_pre, w.coef, w.dcv,
+                     w.status);
   return hipGetLastError();
 }
 

@@ -99,15 +99,21 @@ __global__ void __launch_bounds__(256) k_destuff(const uint8_t *__restrict__ dat
     int ktot, rtot;
     int kex = block_excl_scan256(__popc(keep), sh_scan, &ktot);
     int rex = block_excl_scan256(__popc(rst), sh_scan, &rtot);
+    // kept byte o of segment r lands at o + kSegPad * r (r clamped so a
+    // stream with surplus RSTn markers stays inside the image's region)
     int64_t o = out_base + kex;
     int r = rst_base + rex;
+    int64_t pad = (int64_t)kSegPad * min(r, d.nseg - 1);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       if (rst & (1u << j)) {
+        if (r < d.nseg - 1)
+          for (int q = 0; q < kSegPad; ++q) out[o + pad + q] = 0;
         ++r;
-        if (r < d.nseg) segs[d.seg_base + r].byte_start = d.dst_off + o;
+        pad = (int64_t)kSegPad * min(r, d.nseg - 1);
+        if (r < d.nseg) segs[d.seg_base + r].byte_start = d.dst_off + o + pad;
       }
-      if (keep & (1u << j)) out[o++] = b[j + 1];
+      if (keep & (1u << j)) out[pad + o++] = b[j + 1];
     }
     out_base += ktot;
     rst_base += rtot;
@@ -117,14 +123,16 @@ __global__ void __launch_bounds__(256) k_destuff(const uint8_t *__restrict__ dat
     if (rst_base != d.nseg - 1) {
       status[img] = 3; // LDT_IMG_CORRUPT: restart markers do not match the header
     }
-    // pad 8 zero bytes after the data so aligned 32-bit reads never see stale bytes
-    for (int j = 0; j < 8; ++j) out[out_base + j] = 0;
+    // zero pad after the last segment
+    const int64_t tail = out_base + (int64_t)kSegPad * min(rst_base, d.nseg - 1);
+    for (int j = 0; j < kSegPad; ++j) out[tail + j] = 0;
   }
   __syncthreads();
-  // segment ends: next segment's start, last = total kept bytes
+  // segment ends: the next segment's start less the pad; last = end of data
   for (int s = tid; s < d.nseg; s += 256) {
-    int64_t e = (s + 1 < d.nseg && rst_base == d.nseg - 1) ? segs[d.seg_base + s + 1].byte_start
-                                                           : d.dst_off + out_base;
+    int64_t e = (s + 1 < d.nseg && rst_base == d.nseg - 1)
+                    ? segs[d.seg_base + s + 1].byte_start - kSegPad
+                    : d.dst_off + out_base + (int64_t)kSegPad * min(rst_base, d.nseg - 1);
     if (rst_base != d.nseg - 1) segs[d.seg_base + s].byte_start = d.dst_off;
     segs[d.seg_base + s].byte_end = e;
   }
@@ -245,6 +253,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
                                               const uint16_t *__restrict__ qtabs,
                                               const int16_t *__restrict__ coef,
+                                              const int16_t *__restrict__ dcv,
                                               uint8_t *__restrict__ planes,
                                               const int32_t *__restrict__ status) {
   __shared__ int32_t ws[4][8 * 72];
@@ -271,8 +280,11 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
       const uint4 q4 = *reinterpret_cast<const uint4 *>(qtabs + d.qt[comp] * 64 + r * 8);
       const int16_t *cv = reinterpret_cast<const int16_t *>(&raw);
       const uint16_t *qv = reinterpret_cast<const uint16_t *>(&q4);
+      // DC: absolute value from k_dc_scan (the coefficient slot is unused)
+      const int32_t c0 = r == 0 ? (int32_t)dcv[d.coef_off + blk] : (int32_t)cv[0];
+      w[r * 8] = c0 * (int32_t)qv[0];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) w[r * 8 + j] = (int32_t)cv[j] * (int32_t)qv[j];
+      for (int j = 1; j < 8; ++j) w[r * 8 + j] = (int32_t)cv[j] * (int32_t)qv[j];
     }
     wave_lds_sync();
     // pass 1: column r of the block (jidctint.c pass 1, with the DC shortcut)
@@ -601,7 +613,8 @@ hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n == 0 || p.max_blocks == 0) return hipSuccess;
   dim3 grid((unsigned)((p.max_blocks + kIdctBlocksPerWg - 1) / kIdctBlocksPerWg), (unsigned)p.n);
-  hipLaunchKernelGGL(k_idct, grid, dim3(256), 0, s, p.descs, p.qtabs, w.coef, w.planes, w.status);
+  hipLaunchKernelGGL(k_idct, grid, dim3(256), 0, s, p.descs, p.qtabs, w.coef, w.dcv, w.planes,
+                     w.status);
   return hipGetLastError();
 }
 

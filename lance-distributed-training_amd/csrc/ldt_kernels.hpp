@@ -40,16 +40,18 @@ struct DevPlan {
 struct DevWork {
   const uint8_t *data;  // compressed cells
   uint8_t *dstuf;       // destuffed entropy data
-  int16_t *coef;        // coefficients
+  int16_t *coef;        // coefficients (the DC slot of each block is unused)
+  int16_t *dcv;         // per block: DC difference (Huffman), then absolute DC (k_dc_scan)
   uint8_t *planes;      // component planes
   int32_t *status;      // per image
   SubState *sub;        // per subsequence thread (n_wg * 256)
-  int32_t *sub_pre;     // exclusive prefix of (nblk, dc0, dc1, dc2) per thread (x4)
+  int32_t *sub_pre;     // exclusive prefix of nblk per thread
 };
 
 hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s);
+hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
                               hipStream_t s);

@@ -2,13 +2,14 @@
 // (ldt_abi.cpp) and the gfx950 kernels (ldt_kernels.hip). Everything here is
 // laid out for one H2D copy of a per-batch "plan" blob into HBM.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace ldt {
 
 constexpr int kOut = 224;            // transforms.Resize((224, 224)) lance_iterable.py:29
 constexpr int kMaxBlocksPerMcu = 10; // T.81 limit for interleaved scans
-constexpr int kLookBits = 9;         // Huffman lookahead (libjpeg HUFF_LOOKAHEAD = 8)
+constexpr int kLookBits = 11;        // first-level Huffman lookup bits (libjpeg HUFF_LOOKAHEAD = 8)
 constexpr int kPrecisionBits = 22;   // Pillow Resample.c PRECISION_BITS = 32 - 8 - 2
 
 // Per-image descriptor, one per row of the batch.
@@ -56,27 +57,53 @@ struct Segment {
 // Per-subsequence-thread decode state of the parallel Huffman decoder.
 struct SubState {
   int32_t exit_p;   // bit position (segment-relative) of the first symbol at/after the range end
-  int32_t exit_bk;  // (b << 8) | k at that symbol
+  int32_t exit_bk;  // (3 * b << 8) | k at that symbol (b: block within the MCU)
   int32_t nblk;     // DC symbols decoded inside the range (blocks started)
-  int32_t dc[3];    // sum of DC differences per component inside the range
+  int32_t pad;
 };
 
 constexpr int kSyncThreads = 256;
-// Lane 0 of every decode workgroup is a helper that warms up on the previous
-// workgroup's last subsequence; lanes 1..255 own subsequence slots.
-constexpr int kSlotsPerWg = kSyncThreads - 1;
+// Lanes 0..kHelpers-1 of every decode workgroup are helpers: they decode the
+// kHelpers subsequences just before the workgroup's first slot, so the first
+// slot's entry state is almost always right before any cross-workgroup fix.
+// Lanes kHelpers..255 own subsequence slots.
+constexpr int kHelpers = 4;
+constexpr int kSlotsPerWg = kSyncThreads - kHelpers;
+// Zero bytes after every destuffed segment (restart interval): a bit reader
+// may look up to 8 bytes past a segment without a bounds check and reads the
+// zeros libjpeg inserts at a marker (jdhuff.c jpeg_fill_bit_buffer).
+constexpr int kSegPad = 8;
 
 // Device Huffman table: jdhuff.c's d_derived_tbl restated as a two-level
-// lookup. l1 is indexed by the next 9 bits: (code_len << 8) | symbol for codes
-// of <= 9 bits; 0x8000 | chunk for longer codes, whose symbol is l2[chunk]
-// indexed by the following 7 bits; 0xFFFF (tables with more than kL2Chunks
-// long-code prefixes) falls back to the canonical maxcode search. An l2 entry
-// of 0 is an invalid code (libjpeg: warning, 16 bits skipped, value 0).
+// lookup over the next 16 bits: l1 by the next kLookBits bits, l2 (chunks of
+// 2^kL2Bits) by the following kL2Bits. Entries are 16 bits:
+//   total (bits 0-4)  code length + extra (magnitude) bits, >= 1
+//   s     (bits 5-8)  extra bits (jdhuff.c s; DC: the symbol, AC: symbol & 15)
+//   adv   (bits 9-15) advance of the coefficient index k: DC 1; AC r + 1 if
+//                     s != 0, 16 for ZRL, 64 for EOB (ends the block)
+// total == 0 marks an indirect l1 entry: s-field = chunk of l2, or
+// 15 = canonical maxcode search (tables
+// with more than kL2Chunks long-code prefixes). Unused codes hold the invalid
+// entry (libjpeg: warning, 16 bits skipped, symbol 0).
 constexpr int kL2Chunks = 8;
-constexpr int kTabU16 = 512 + kL2Chunks * 128; // uint16 entries per table in LDS
+constexpr int kL2Bits = 16 - kLookBits;
+constexpr int kTabU16 = (1 << kLookBits) + (kL2Chunks << kL2Bits); // uint16 entries per table
+constexpr uint32_t kHuffCanon = 15u << 5;
+__host__ __device__ inline uint16_t huff_entry(int len, int sym, bool dc) {
+  int s, adv;
+  if (dc) {
+    s = sym;
+    adv = 1;
+  } else {
+    s = sym & 15;
+    const int r = sym >> 4;
+    adv = s ? r + 1 : (r == 15 ? 16 : 64);
+  }
+  return (uint16_t)((len + s) | (s << 5) | (adv << 9));
+}
 struct HuffTab {
-  uint16_t l1[512];
-  uint16_t l2[kL2Chunks * 128];
+  uint16_t l1[1 << kLookBits];
+  uint16_t l2[kL2Chunks << kL2Bits];
   int32_t maxcode[18]; // [l] largest code of length l (-1 none), [17] sentinel
   int32_t valoff[18];
   uint8_t vals[256];
