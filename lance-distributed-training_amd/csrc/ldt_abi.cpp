@@ -271,7 +271,7 @@ struct ldt_ctx {
   bool sync_status = true;
   int huff_mode = 0;
   int subseq_bits = 1024;
-  DevBuf d_data, d_plan, d_dstuf, d_coef, d_planes, d_raw, d_sub, d_pre;
+  DevBuf d_data, d_plan, d_dstuf, d_coef, d_planes, d_raw, d_sub, d_pre, d_dscnt;
   static constexpr int kSlots = 2;
   PinBuf h_data[kSlots], h_plan[kSlots];
   hipEvent_t slot_ev[kSlots] = {nullptr, nullptr};
@@ -462,6 +462,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   const int SB = c->subseq_bits;
   int32_t n_wg = 0;
   std::vector<int32_t> wg_img;
+  int32_t n_chunks = 0;          // destuff chunks (kDsChunk bytes of scan data each)
+  std::vector<int32_t> chunk_img;
   int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3, max_tabs = 1;
   bool any_bad = false;
   for (int64_t i = 0; i < n; ++i) {
@@ -641,6 +643,11 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       for (int q = 0; q < d.wg_count; ++q) wg_img.push_back((int32_t)i);
       n_wg += d.wg_count;
     }
+    // destuff chunks over the scan bytes from the 4-aligned word before them
+    d.ds_first = n_chunks;
+    d.ds_count = (int32_t)((d.src_len + 3 + kDsChunkBytes - 1) / kDsChunkBytes);
+    for (int q = 0; q < d.ds_count; ++q) chunk_img.push_back((int32_t)i);
+    n_chunks += d.ds_count;
     d.dst_off = dst_total;
     dst_total += align_up(d.src_len + 16 + (int64_t)kSegPad * d.nseg, 16);
     d.coef_off = coef_blocks;
@@ -678,6 +685,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   off = align_up(off + 4 * n, 64);
   const int64_t off_wg = off;
   off = align_up(off + 4 * (int64_t)n_wg, 64);
+  const int64_t off_chunk = off;
+  off = align_up(off + 4 * (int64_t)n_chunks, 64);
   const int64_t off_redo = off;
   off = align_up(off + 64, 64);
   const int64_t plan_bytes = off;
@@ -702,6 +711,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if (labels) memcpy(hp + ph.off_labels, labels + label_offset, 8 * (size_t)n);
   memcpy(hp + off_status, st.data(), 4 * (size_t)n);
   if (n_wg) memcpy(hp + off_wg, wg_img.data(), 4 * (size_t)n_wg);
+  if (n_chunks) memcpy(hp + off_chunk, chunk_img.data(), 4 * (size_t)n_chunks);
   memset(hp + off_redo, 0, 64);
 
   // ---- device workspace ----
@@ -709,6 +719,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 130 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
+  if ((rc = ensure_dev(c, c->d_dscnt, 16 * (size_t)(n_chunks + 1), s))) return rc;
   if (parallel && n_wg) {
     const size_t slots = (size_t)n_wg * kSyncThreads;
     if ((rc = ensure_dev(c, c->d_sub, slots * sizeof(SubState), s))) return rc;
@@ -748,6 +759,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.subseq_bits = parallel ? SB : 0;
   p.n_wg = parallel ? n_wg : 0;
   p.wg_img = reinterpret_cast<const int32_t *>(dp + off_wg);
+  p.n_chunks = n_chunks;
+  p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
   p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
   p.max_tabs = max_tabs;
   c->last_off_redo = off_redo;
@@ -759,6 +772,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.planes = static_cast<uint8_t *>(c->d_planes.p);
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
   w.sub = static_cast<SubState *>(c->d_sub.p);
+  w.ds_cnt = static_cast<int4 *>(c->d_dscnt.p);
   w.sub_pre = static_cast<int32_t *>(c->d_pre.p);
 
   HIPCHK(c, launch_destuff(p, w, s));
@@ -842,7 +856,7 @@ void ldt_destroy(ldt_ctx *c) {
   DeviceGuard g(c->device);
   (void)hipDeviceSynchronize();
   DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_planes, &c->d_raw,
-                    &c->d_sub, &c->d_pre};
+                    &c->d_sub, &c->d_pre, &c->d_dscnt};
   for (DevBuf *b : dbs)
     if (b->p) (void)hipFree(b->p);
   for (int k = 0; k < ldt_ctx::kSlots; ++k) {

@@ -54,9 +54,13 @@ extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
 // followed by kSegPad zero bytes, and a symbol starting before the segment end
 // reads at most 31 bits from its start.
 // ---------------------------------------------------------------------------
+// The LDS window is skewed by one word per 32 (word i at i + i/32): lanes'
+// ranges start S/8 bytes apart, which would otherwise map every lane to the
+// same few banks.
+__device__ __forceinline__ int32_t skew(int32_t i) { return i + (i >> 5); }
 struct LdsWords {
   lds_cu32 w;
-  __device__ __forceinline__ uint32_t operator()(int32_t i) const { return w[i]; }
+  __device__ __forceinline__ uint32_t operator()(int32_t i) const { return w[skew(i)]; }
 };
 struct GlobWords {
   const uint32_t *w; // 4-aligned
@@ -427,12 +431,18 @@ hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
 // only counts blocks per range; k_huff_write then decodes every range from its
 // true entry and k_dc_scan adds the DC predictors.
 //
-// LDS window: the workgroup's destuffed bytes, byte-swapped. Without restart
-// markers they span 256 * S/8 + 76 bytes; a workgroup whose ranges span more
-// (many small restart segments, kSegPad apart) reads global memory instead.
+// LDS window: the workgroup's destuffed bytes, byte-swapped and skewed. Without
+// restart markers they span 256 * S/8 + 76 bytes; a workgroup whose ranges
+// span more (many small restart segments, kSegPad apart) reads global memory
+// instead. LDS per workgroup stays under a third of the CU's 160 KB at S = 1024
+// with four tables, so three decode workgroups share a CU.
 // ===========================================================================
 
-__host__ __device__ inline int window_bytes(int S) { return 256 * (S / 8) + 512; }
+__host__ __device__ inline int window_bytes(int S) { return 256 * (S / 8) + 128; }
+__host__ __device__ inline int window_lds_bytes(int S) {
+  const int words = window_bytes(S) / 4;
+  return ((words + words / 32 + 1) * 4 + 15) & ~15;
+}
 
 // Locate the segment that owns image-local slot `lt` (sub_first ascending).
 __device__ __forceinline__ int find_segment(const Segment *__restrict__ segs, int seg_base, int nseg,
@@ -521,7 +531,7 @@ __device__ __forceinline__ Dec sub_setup(const ImgDesc &d, const Segment *__rest
   sc.in_lds = nbytes <= window_bytes(S);
   sc.gw = reinterpret_cast<const uint32_t *>(dstuf + wb);
   if (sc.in_lds)
-    for (int i = tid; i < (int)nbytes / 4; i += kSyncThreads) win[i] = __builtin_bswap32(sc.gw[i]);
+    for (int i = tid; i < (int)nbytes / 4; i += kSyncThreads) win[skew(i)] = __builtin_bswap32(sc.gw[i]);
   sc.pbias = (int32_t)(seg0 - wb) * 8;
   __syncthreads();
   return dec;
@@ -590,7 +600,8 @@ __device__ __forceinline__ bool count_run(Rd<W> &R, int32_t range_start, int32_t
 }
 
 struct SyncLds {
-  int32_t ex_p[kSyncThreads], ex_bk[kSyncThreads];
+  int32_t ex_p[kSyncThreads];
+  uint16_t ex_bk[kSyncThreads]; // (3b << 8) | k <= 27 * 256 + 63
   uint8_t chg[kSyncThreads];
   int any_changed;
 };
@@ -615,7 +626,7 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
     R.seek(rstart);
     count_run<false>(R, rstart, stop, S, st, dec, nblk, cp, none, 0);
     sh.ex_p[tid] = R.p - sc.pbias;
-    sh.ex_bk[tid] = st.bk();
+    sh.ex_bk[tid] = (uint16_t)st.bk();
   } else {
     sh.ex_p[tid] = 0;
     sh.ex_bk[tid] = 0;
@@ -649,7 +660,7 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
     sh.chg[tid] = changed ? 1 : 0;
     if (changed) {
       sh.ex_p[tid] = np;
-      sh.ex_bk[tid] = nbk;
+      sh.ex_bk[tid] = (uint16_t)nbk;
       sh.any_changed = 1;
     }
     __syncthreads();
@@ -678,7 +689,7 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
   SubCtx sc;
   const lds_u32 win = (lds_u32)dyn_lds;
   const Dec dec = sub_setup(d, segs, htabs, S, dstuf, win,
-                            (lds_u16)(dyn_lds + window_bytes(S) / 4), sh_lohi, sc);
+                            (lds_u16)(dyn_lds + window_lds_bytes(S) / 4), sh_lohi, sc);
   int nblk;
   if (sc.in_lds) nblk = sync_lane(LdsWords{(lds_cu32)win}, sc, dec, S, sh, dbg);
   else nblk = sync_lane(GlobWords{sc.gw}, sc, dec, S, sh, dbg);
@@ -864,7 +875,7 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
   SubCtx sc;
   const lds_u32 win = (lds_u32)dyn_lds;
   const Dec dec = sub_setup(d, segs, htabs, S, dstuf, win,
-                            (lds_u16)(dyn_lds + window_bytes(S) / 4), sh_lohi, sc);
+                            (lds_u16)(dyn_lds + window_lds_bytes(S) / 4), sh_lohi, sc);
   if (!sc.active) return;
   const Segment &sg = segs[sc.seg];
   const int64_t gt = (int64_t)blockIdx.x * kSyncThreads + tid;
@@ -887,7 +898,7 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_wg == 0) return hipSuccess;
   const size_t tab_lds = (size_t)(p.max_tabs < 1 ? 1 : p.max_tabs) * kTabU16 * 2;
-  const size_t dec_lds = (size_t)window_bytes(p.subseq_bits) + tab_lds;
+  const size_t dec_lds = (size_t)window_lds_bytes(p.subseq_bits) + tab_lds;
   hipLaunchKernelGGL(k_huff_sync, dim3(p.n_wg), dim3(kSyncThreads), dec_lds, s, p.descs, p.segs,
                      p.htabs, w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.status, p.redo);
   hipLaunchKernelGGL(k_huff_fix, dim3(p.n_wg), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,

@@ -30,94 +30,260 @@
 namespace ldt {
 
 // ---------------------------------------------------------------------------
-// k_destuff: one 256-thread workgroup per image, 16 bytes per thread per pass.
+// Destuff: jdhuff.c jpeg_fill_bit_buffer / jdmarker.c semantics over the
+// entropy-coded bytes of each cell — FF00 -> FF, FF fill bytes dropped, RSTn
+// ends a segment, any other marker ends the scan. Kept bytes are compacted per
+// image; every segment is followed by kSegPad zero bytes.
+//   k_destuff_count   one workgroup per 4 KB chunk: kept bytes, RSTn markers,
+//                     end marker seen;
+//   k_destuff_write   one workgroup per chunk: output offset from the image's
+//                     earlier chunks, classify again, compact in LDS, copy out;
+//   k_destuff_layout  one workgroup per image: segment ends, the final pad, the
+//                     parallel decoder's subsequence layout.
+// Chunks run over 4-aligned source words (B0 = cell scan start rounded down):
+// chunk byte k of chunk c is relative position c * kDsChunk + k - lead.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_destuff(const uint8_t *__restrict__ data,
-                                                 const ImgDesc *__restrict__ descs,
-                                                 Segment *__restrict__ segs,
-                                                 uint8_t *__restrict__ dst,
-                                                 int32_t *__restrict__ status, int subseq_bits) {
-  const int img = blockIdx.x;
-  const ImgDesc &d = descs[img];
-  if (status[img] != 0) return;
+constexpr int kDsChunk = kDsChunkBytes;        // 16 bytes per lane
+constexpr int kDsWords = kDsChunk / 4 + 2;     // + the words before and after
+constexpr int kDsInLds = kDsWords + kDsWords / 8 + 1;
+// LDS output of one chunk: kept bytes + kSegPad per RSTn (2 input bytes each) + alignment
+constexpr int kDsOutLds = (kDsChunk + kSegPad * (kDsChunk / 2)) / 4 + 4;
+
+__device__ __forceinline__ int ds_skew(int w) { return w + (w >> 3); }
+
+struct DsChunk {
+  const uint8_t *B0;
+  int lead;
+  int64_t span;  // bytes from B0 to the end of the cell
+  int64_t cb;    // chunk start (bytes from B0)
+};
+
+__device__ __forceinline__ DsChunk ds_chunk(const uint8_t *data, const ImgDesc &d, int lc) {
+  DsChunk k;
+  const uint8_t *src = data + d.src_off;
+  k.B0 = reinterpret_cast<const uint8_t *>((uintptr_t)src & ~(uintptr_t)3);
+  k.lead = (int)(src - k.B0);
+  k.span = d.src_len + k.lead;
+  k.cb = (int64_t)lc * kDsChunk;
+  return k;
+}
+
+// Stage the chunk's words (and one on each side) into LDS, zero outside the cell.
+__device__ __forceinline__ void ds_stage(const DsChunk &k, uint32_t *s_in, int tid) {
+  const uint32_t *wsrc = reinterpret_cast<const uint32_t *>(k.B0 + k.cb) - 1;
+  const int64_t nwords_cell = (k.span - k.cb + 3) / 4 + 1; // words touching the cell
+  for (int w = tid; w < kDsWords; w += 256) {
+    uint32_t v = 0;
+    if (w < nwords_cell && (k.cb > 0 || w > 0)) v = wsrc[w];
+    s_in[ds_skew(w)] = v;
+  }
+}
+
+// Classify lane tid's 16 bytes (after the LDS stage and a barrier).
+__device__ __forceinline__ void ds_classify(const uint32_t *s_in, const DsChunk &k, int64_t L, int tid,
+                                            uint32_t wv[6], uint32_t &keep, uint32_t &rst,
+                                            int &local_end) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) wv[i] = s_in[ds_skew(4 * tid + i)];
+  const int64_t p0 = k.cb + 16 * tid - k.lead;
+  keep = rst = 0;
+  local_end = 16;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t p = p0 + j;
+    const uint32_t prev = (wv[(j + 3) >> 2] >> (8 * ((j + 3) & 3))) & 255;
+    const uint32_t cur = (wv[(j + 4) >> 2] >> (8 * ((j + 4) & 3))) & 255;
+    const uint32_t next = (wv[(j + 5) >> 2] >> (8 * ((j + 5) & 3))) & 255;
+    const bool in = p >= 0 && p < L;
+    const bool next_in = p + 1 < L;
+    bool drop = false;
+    if (cur == 0xFF) {
+      const uint32_t nx = next_in ? next : 0u;
+      if (nx == 0x00) {
+        drop = false;                        // stuffed data byte 0xFF
+      } else if (nx == 0xFF || (nx >= 0xD0 && nx <= 0xD7)) {
+        drop = true;                         // fill byte or RSTn prefix
+      } else if (in && next_in) {
+        if (local_end == 16) local_end = j;  // end-of-scan marker
+        drop = true;
+      } else {
+        drop = true;                         // trailing 0xFF at end of cell
+      }
+    } else if (prev == 0xFF && p > 0) {
+      if (cur == 0x00) drop = true;          // stuffing zero
+      else if (cur >= 0xD0 && cur <= 0xD7) {
+        drop = true;
+        if (in) rst |= 1u << j;              // RSTn code: segment boundary
+      }
+    }
+    if (in && !drop) keep |= 1u << j;
+  }
+}
+
+// Limit the lane's masks to bytes before the chunk's end marker (sh_end).
+__device__ __forceinline__ void ds_limit(int cend, int tid, uint32_t &keep, uint32_t &rst) {
+  const int my_lo = tid * 16;
+  const uint32_t lim = (cend <= my_lo) ? 0u : (cend - my_lo >= 16 ? 0xFFFFu : ((1u << (cend - my_lo)) - 1u));
+  keep &= lim;
+  rst &= lim;
+}
+
+__global__ void __launch_bounds__(256) k_destuff_count(const uint8_t *__restrict__ data,
+                                                       const ImgDesc *__restrict__ descs,
+                                                       const int32_t *__restrict__ chunk_img,
+                                                       int4 *__restrict__ cnt,
+                                                       const int32_t *__restrict__ status) {
+  __shared__ uint32_t s_in[kDsInLds];
   __shared__ int sh_scan[8];
   __shared__ int sh_end;
-  const int tid = threadIdx.x;
-  const uint8_t *src = data + d.src_off;
-  const int64_t L = d.src_len;
-  uint8_t *out = dst + d.dst_off;
-  int64_t out_base = 0;   // kept bytes so far
-  int rst_base = 0;       // RST markers so far
-  bool done = false;
-  for (int64_t chunk = 0; chunk < L && !done; chunk += 256 * 16) {
-    const int64_t p0 = chunk + (int64_t)tid * 16;
-    uint8_t b[18];
-    // b[0] = byte before p0, b[1..16] = bytes p0..p0+15, b[17] = byte after
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int img = chunk_img[c];
+  const ImgDesc &d = descs[img];
+  const DsChunk k = ds_chunk(data, d, c - d.ds_first);
+  if (status[img] != 0 || k.cb >= k.span) {
+    if (tid == 0) cnt[c] = make_int4(0, 0, 0, 0);
+    return;
+  }
+  ds_stage(k, s_in, tid);
+  if (tid == 0) sh_end = kDsChunk;
+  __syncthreads();
+  uint32_t wv[6], keep, rst;
+  int local_end;
+  ds_classify(s_in, k, d.src_len, tid, wv, keep, rst, local_end);
+  if (local_end < 16) atomicMin(&sh_end, tid * 16 + local_end);
+  __syncthreads();
+  const int cend = sh_end;
+  ds_limit(cend, tid, keep, rst);
+  int ktot, rtot;
+  (void)block_excl_scan256(__popc(keep), sh_scan, &ktot);
+  (void)block_excl_scan256(__popc(rst), sh_scan, &rtot);
+  if (tid == 0) cnt[c] = make_int4(ktot, rtot, cend < kDsChunk ? 1 : 0, 0);
+}
+
+__device__ __forceinline__ void lds_put8(uint32_t *buf, int pos, uint32_t v) {
+  reinterpret_cast<uint8_t *>(buf)[pos] = (uint8_t)v;
+}
+
+__global__ void __launch_bounds__(256) k_destuff_write(const uint8_t *__restrict__ data,
+                                                       const ImgDesc *__restrict__ descs,
+                                                       Segment *__restrict__ segs,
+                                                       const int32_t *__restrict__ chunk_img,
+                                                       const int4 *__restrict__ cnt,
+                                                       uint8_t *__restrict__ dst,
+                                                       const int32_t *__restrict__ status) {
+  __shared__ uint32_t s_in[kDsInLds];
+  __shared__ __attribute__((aligned(16))) uint32_t s_out[kDsOutLds];
+  __shared__ int sh_scan[8];
+  __shared__ int sh_end;
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int img = chunk_img[c];
+  const ImgDesc &d = descs[img];
+  const DsChunk k = ds_chunk(data, d, c - d.ds_first);
+  if (status[img] != 0 || k.cb >= k.span) return;
+  // output offset: kept bytes and RSTn markers of the image's earlier chunks
+  int kb = 0, rb = 0, ended = 0;
+  for (int q = d.ds_first + tid; q < c; q += 256) {
+    const int4 v = cnt[q];
+    kb += v.x;
+    rb += v.y;
+    ended |= v.z;
+  }
+  int tmp;
+  (void)block_excl_scan256(kb, sh_scan, &kb);
+  (void)block_excl_scan256(rb, sh_scan, &rb);
+  (void)block_excl_scan256(ended, sh_scan, &tmp);
+  if (tmp != 0) return; // after the end-of-scan marker
+  ds_stage(k, s_in, tid);
+  if (tid == 0) sh_end = kDsChunk;
+  __syncthreads();
+  uint32_t wv[6], keep, rst;
+  int local_end;
+  ds_classify(s_in, k, d.src_len, tid, wv, keep, rst, local_end);
+  if (local_end < 16) atomicMin(&sh_end, tid * 16 + local_end);
+  __syncthreads();
+  ds_limit(sh_end, tid, keep, rst);
+  int ktot, rtot;
+  const int kex = block_excl_scan256(__popc(keep), sh_scan, &ktot);
+  const int rex = block_excl_scan256(__popc(rst), sh_scan, &rtot);
+  // kept byte o of segment r lands at o + kSegPad * r (r clamped so a stream
+  // with surplus RSTn markers stays inside the image's region)
+  const int last = d.nseg - 1;
+  const int64_t g0 = kb + (int64_t)kSegPad * min(rb, last); // chunk output start (image-relative)
+  const int64_t gal = g0 & ~(int64_t)3;                      // s_out byte 0
+  const int rpads = min(rb + rtot, last) - min(rb, last);
+  const int lo_b = (int)(g0 - gal);
+  const int gend = lo_b + ktot + kSegPad * rpads;
+  int r = rb + rex;
+  int o = lo_b + kex + kSegPad * (min(r, last) - min(rb, last));
+  if (keep == 0xFFFFu) {
+    // all 16 bytes kept, no marker: a byte-shifted copy of the input run
+    const int a = o & 3, w0 = o >> 2;
+    if (a == 0) {
 #pragma unroll
-    for (int j = 0; j < 18; ++j) {
-      int64_t p = p0 - 1 + j;
-      b[j] = (p >= 0 && p < L) ? src[p] : 0;
-    }
-    uint32_t keep = 0, rst = 0;
-    int local_end = 16;
+      for (int q = 0; q < 4; ++q) s_out[w0 + q] = wv[1 + q];
+    } else {
+      for (int q = 0; q < 4 - a; ++q) lds_put8(s_out, o + q, wv[1] >> (8 * q));
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t p = p0 + j;
-      const uint8_t prev = b[j], cur = b[j + 1], next = b[j + 2];
-      bool in = p < L;
-      bool drop = false;
-      if (cur == 0xFF) {
-        if (next == 0x00) {
-          drop = false;                       // stuffed data byte 0xFF
-        } else if (next == 0xFF || (next >= 0xD0 && next <= 0xD7)) {
-          drop = true;                        // fill byte or RSTn prefix
-        } else if (in && p + 1 < L) {
-          if (local_end == 16) local_end = j; // end-of-scan marker
-          drop = true;
-        } else {
-          drop = true;                        // trailing 0xFF at end of cell
-        }
-      } else if (prev == 0xFF && p > 0) {
-        if (cur == 0x00) drop = true;         // stuffing zero
-        else if (cur >= 0xD0 && cur <= 0xD7) {
-          drop = true;
-          if (in) rst |= 1u << j;             // RSTn code: segment boundary
-        }
-      }
-      if (in && !drop) keep |= 1u << j;
+      for (int q = 0; q < 3; ++q)
+        s_out[w0 + 1 + q] = __builtin_amdgcn_alignbyte(wv[2 + q], wv[1 + q], (uint32_t)(4 - a));
+      for (int q = 0; q < a; ++q) lds_put8(s_out, 4 * (w0 + 4) + q, wv[4] >> (8 * (4 - a + q)));
     }
-    if (tid == 0) sh_end = 256 * 16;
-    __syncthreads();
-    if (local_end < 16) atomicMin(&sh_end, tid * 16 + local_end);
-    __syncthreads();
-    const int cend = sh_end;
-    if (cend < 256 * 16) done = true;
-    const int my_lo = tid * 16;
-    uint32_t lim = (cend <= my_lo) ? 0u : (cend - my_lo >= 16 ? 0xFFFFu : ((1u << (cend - my_lo)) - 1u));
-    keep &= lim;
-    rst &= lim;
-    int ktot, rtot;
-    int kex = block_excl_scan256(__popc(keep), sh_scan, &ktot);
-    int rex = block_excl_scan256(__popc(rst), sh_scan, &rtot);
-    // kept byte o of segment r lands at o + kSegPad * r (r clamped so a
-    // stream with surplus RSTn markers stays inside the image's region)
-    int64_t o = out_base + kex;
-    int r = rst_base + rex;
-    int64_t pad = (int64_t)kSegPad * min(r, d.nseg - 1);
+  } else {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       if (rst & (1u << j)) {
-        if (r < d.nseg - 1)
-          for (int q = 0; q < kSegPad; ++q) out[o + pad + q] = 0;
+        if (r < last) {
+          for (int q = 0; q < kSegPad; ++q) lds_put8(s_out, o + q, 0u);
+          o += kSegPad;
+        }
         ++r;
-        pad = (int64_t)kSegPad * min(r, d.nseg - 1);
-        if (r < d.nseg) segs[d.seg_base + r].byte_start = d.dst_off + o + pad;
+        if (r < d.nseg) segs[d.seg_base + r].byte_start = d.dst_off + gal + o;
       }
-      if (keep & (1u << j)) out[pad + o++] = b[j + 1];
+      if (keep & (1u << j)) lds_put8(s_out, o++, wv[(j + 4) >> 2] >> (8 * ((j + 4) & 3)));
     }
-    out_base += ktot;
-    rst_base += rtot;
   }
+  __syncthreads();
+  uint8_t *out = dst + d.dst_off;
+  for (int w = tid; 4 * w < gend; w += 256) {
+    const int b0 = 4 * w;
+    if (b0 >= lo_b && b0 + 4 <= gend) {
+      *reinterpret_cast<uint32_t *>(out + gal + b0) = s_out[w];
+    } else {
+      for (int q = 0; q < 4; ++q)
+        if (b0 + q >= lo_b && b0 + q < gend)
+          out[gal + b0 + q] = reinterpret_cast<const uint8_t *>(s_out)[b0 + q];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restrict__ descs,
+                                                        Segment *__restrict__ segs,
+                                                        const int4 *__restrict__ cnt,
+                                                        uint8_t *__restrict__ dst,
+                                                        int32_t *__restrict__ status,
+                                                        int subseq_bits) {
+  __shared__ int sh_scan[8];
+  __shared__ int sh_endc;
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const ImgDesc &d = descs[img];
+  if (status[img] != 0) return;
+  // chunks up to and including the first one holding the end-of-scan marker
+  if (tid == 0) sh_endc = d.ds_count;
+  __syncthreads();
+  for (int q = tid; q < d.ds_count; q += 256)
+    if (cnt[d.ds_first + q].z) atomicMin(&sh_endc, q + 1);
+  __syncthreads();
+  const int nch = sh_endc;
+  int kt = 0, rt = 0;
+  for (int q = tid; q < nch; q += 256) {
+    kt += cnt[d.ds_first + q].x;
+    rt += cnt[d.ds_first + q].y;
+  }
+  (void)block_excl_scan256(kt, sh_scan, &kt);
+  (void)block_excl_scan256(rt, sh_scan, &rt);
+  const int64_t out_base = kt;
+  const int rst_base = rt;
+  uint8_t *out = dst + d.dst_off;
   if (tid == 0) {
     segs[d.seg_base].byte_start = d.dst_off;
     if (rst_base != d.nseg - 1) {
@@ -143,18 +309,18 @@ __global__ void __launch_bounds__(256) k_destuff(const uint8_t *__restrict__ dat
   int base = 0;
   for (int s0 = 0; s0 < d.nseg; s0 += 256) {
     const int s = s0 + tid;
-    int cnt = 0;
+    int cnt_s = 0;
     if (s < d.nseg) {
       const Segment &sg = segs[d.seg_base + s];
       const int64_t bits = (sg.byte_end - sg.byte_start) * 8;
-      cnt = (int)((bits + subseq_bits - 1) / subseq_bits);
-      if (cnt < 1) cnt = 1;
+      cnt_s = (int)((bits + subseq_bits - 1) / subseq_bits);
+      if (cnt_s < 1) cnt_s = 1;
     }
     int tot;
-    const int ex = block_excl_scan256(cnt, sh_scan, &tot);
+    const int ex = block_excl_scan256(cnt_s, sh_scan, &tot);
     if (s < d.nseg) {
       segs[d.seg_base + s].sub_first = base + ex;
-      segs[d.seg_base + s].sub_count = cnt;
+      segs[d.seg_base + s].sub_count = cnt_s;
     }
     base += tot;
   }
@@ -605,8 +771,14 @@ __global__ void __launch_bounds__(256) k_shard_fragments(const int64_t *frag_row
 // ---------------------------------------------------------------------------
 hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_destuff, dim3(p.n), dim3(256), 0, s, w.data, p.descs, p.segs, w.dstuf,
-                     w.status, p.subseq_bits);
+  if (p.n_chunks > 0) {
+    hipLaunchKernelGGL(k_destuff_count, dim3(p.n_chunks), dim3(256), 0, s, w.data, p.descs,
+                       p.chunk_img, w.ds_cnt, w.status);
+    hipLaunchKernelGGL(k_destuff_write, dim3(p.n_chunks), dim3(256), 0, s, w.data, p.descs, p.segs,
+                       p.chunk_img, w.ds_cnt, w.dstuf, w.status);
+  }
+  hipLaunchKernelGGL(k_destuff_layout, dim3(p.n), dim3(256), 0, s, p.descs, p.segs, w.ds_cnt,
+                     w.dstuf, w.status, p.subseq_bits);
   return hipGetLastError();
 }
 

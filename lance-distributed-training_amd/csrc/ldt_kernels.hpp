@@ -35,6 +35,9 @@ struct DevPlan {
   const int32_t *wg_img; // workgroup -> image
   int32_t *redo;         // set when a workgroup-boundary walk did not converge
   int max_tabs;          // max distinct Huffman tables of one image (LDS slots)
+  // destuff chunks (4 KB of entropy-coded bytes each)
+  int n_chunks;
+  const int32_t *chunk_img; // chunk -> image
 };
 
 struct DevWork {
@@ -46,6 +49,7 @@ struct DevWork {
   int32_t *status;      // per image
   SubState *sub;        // per subsequence thread (n_wg * 256)
   int32_t *sub_pre;     // exclusive prefix of nblk per thread
+  int4 *ds_cnt;         // per destuff chunk: kept bytes, RSTn markers, end marker seen
 };
 
 hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s);

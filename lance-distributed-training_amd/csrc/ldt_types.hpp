@@ -39,6 +39,8 @@ struct ImgDesc {
   // workgroups [wg_first, wg_first + wg_count) (256 threads each)
   int32_t wg_first, wg_count;
   int32_t sub_cap;   // thread slots reserved (>= sum of segment sub_count)
+  // destuff: this image's 4 KB chunks are [ds_first, ds_first + ds_count)
+  int32_t ds_first, ds_count;
   int32_t pad2_;
 };
 
@@ -67,12 +69,14 @@ constexpr int kSyncThreads = 256;
 // kHelpers subsequences just before the workgroup's first slot, so the first
 // slot's entry state is almost always right before any cross-workgroup fix.
 // Lanes kHelpers..255 own subsequence slots.
-constexpr int kHelpers = 4;
+constexpr int kHelpers = 8;
 constexpr int kSlotsPerWg = kSyncThreads - kHelpers;
 // Zero bytes after every destuffed segment (restart interval): a bit reader
 // may look up to 8 bytes past a segment without a bounds check and reads the
 // zeros libjpeg inserts at a marker (jdhuff.c jpeg_fill_bit_buffer).
 constexpr int kSegPad = 8;
+// Destuff work unit: bytes of entropy-coded data per workgroup.
+constexpr int kDsChunkBytes = 4096;
 
 // Device Huffman table: jdhuff.c's d_derived_tbl restated as a two-level
 // lookup over the next 16 bits: l1 by the next kLookBits bits, l2 (chunks of
