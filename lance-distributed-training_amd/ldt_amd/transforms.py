@@ -262,15 +262,17 @@ class ResidentBatch:
         self.labels = None if labels is None else np.ascontiguousarray(np.asarray(list(labels), np.int64))
         self.bytes = int(self.offsets[-1])
 
-    def decode(self, out=None, out_lbl=None, normalize=None):
-        ctx = self.dec.ctx
+    def decode(self, out=None, out_lbl=None, normalize=None, *, ctx=None, stream=None):
+        """Decode on `stream` (default: the current stream) with context `ctx`
+        (default: the device's shared context)."""
+        ctx = ctx or self.dec.ctx
+        s = stream or torch.cuda.current_stream(self.dec.device)
         if out is None:
             out = torch.empty((self.n, 3, _OUT, _OUT), dtype=torch.float32, device=self.dec.device)
         if self.labels is not None and out_lbl is None:
             out_lbl = torch.empty((self.n,), dtype=torch.int64, device=self.dec.device)
         status = np.zeros(self.n, np.int32)
         norm = _norm_struct(normalize)
-        s = torch.cuda.current_stream(self.dec.device)
         rc = ctx.lib.ldt_decode_batch_resident(
             ctx.handle, self.host.ctypes.data, self.dev.data_ptr(), self.offsets.ctypes.data, self.n,
             self.labels.ctypes.data if self.labels is not None else None,
@@ -280,3 +282,67 @@ class ResidentBatch:
             raise ImageDecodeError({int(i): int(status[i]) for i in np.nonzero(status)[0]})
         ctx.check(rc, "ldt_decode_batch_resident")
         return out, out_lbl
+
+
+class DecodePipeline:
+    """`depth` batches in flight: each slot owns a libldt context (its own HBM
+    workspace and pinned staging ring) and a HIP stream. ``decode(batch)``
+    enqueues on the next slot's stream without waiting for the caller's stream
+    and makes the caller's current stream wait for the result, so the
+    latency-bound Huffman stages of one batch overlap the resize/IDCT of the
+    previous one — the GPU-side analogue of the reference DataLoader's
+    prefetching workers (lance_map_style.py:137, num_workers=8).
+
+    Errors are asynchronous: ``check()`` waits for the most recent batch of
+    every slot and raises ImageDecodeError with its failing rows (per-image
+    status, as ldt_fetch_status reports)."""
+
+    def __init__(self, depth: int = 2, device=None, profile: bool = False):
+        self.dec = _decoder(device)
+        self.depth = max(1, int(depth))
+        self.ctxs = [_lib.Context(self.dec.device.index) for _ in range(self.depth)]
+        for c in self.ctxs:
+            c.set_option(_lib.OPT_SYNC_STATUS, 0)
+            if profile:
+                c.set_option(_lib.OPT_PROFILE, 1)
+        self.streams = [torch.cuda.Stream(self.dec.device) for _ in range(self.depth)]
+        self.sizes = [0] * self.depth
+        self.k = 0
+
+    def decode(self, batch: "ResidentBatch", normalize=None):
+        slot = self.k % self.depth
+        self.k += 1
+        s = self.streams[slot]
+        cur = torch.cuda.current_stream(self.dec.device)
+        with torch.cuda.stream(s):
+            out = torch.empty((batch.n, 3, _OUT, _OUT), dtype=torch.float32, device=self.dec.device)
+            lbl = (torch.empty((batch.n,), dtype=torch.int64, device=self.dec.device)
+                   if batch.labels is not None else None)
+        batch.decode(out, lbl, normalize, ctx=self.ctxs[slot], stream=s)
+        self.sizes[slot] = batch.n
+        cur.wait_stream(s)
+        out.record_stream(cur)
+        if lbl is not None:
+            lbl.record_stream(cur)
+        return out, lbl
+
+    def stage_times(self, reset: bool = False):
+        tot: dict = {}
+        for c in self.ctxs:
+            for k, (ms, n) in c.stage_times(reset=reset).items():
+                a = tot.get(k, (0.0, 0))
+                tot[k] = (a[0] + ms, a[1] + n)
+        return tot
+
+    def check(self):
+        bad = {}
+        for c, s, n in zip(self.ctxs, self.streams, self.sizes):
+            if n == 0:
+                continue
+            st = np.zeros(n, np.int32)
+            rc = c.lib.ldt_fetch_status(c.handle, s.cuda_stream, st.ctypes.data, n)
+            if rc != _lib.LDT_ERR_IMAGE:
+                c.check(rc, "ldt_fetch_status")
+            bad.update({int(i): int(st[i]) for i in np.nonzero(st)[0]})
+        if bad:
+            raise ImageDecodeError(bad)

@@ -220,6 +220,33 @@ def test_resident_batch_and_determinism():
         _check(a[k].cpu().numpy(), oracle.jpeg_to_tensor(cells[k]), f"resident[{k}]")
 
 
+def test_decode_pipeline_overlapping_batches():
+    """DecodePipeline: batches in flight on separate streams/contexts decode
+    exactly like the single-stream path; errors surface through check()."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import synth
+
+    c2, l2 = synth.q90_512(48, seed=21)
+    c4, l4 = synth.imagenet_like(40, seed=22)
+    batches = [ldt_amd.ResidentBatch(c2, l2), ldt_amd.ResidentBatch(c4, l4)]
+    ref = [b.decode() for b in batches]
+    pipe = ldt_amd.DecodePipeline(depth=2)
+    outs = [pipe.decode(batches[k % 2]) for k in range(6)]
+    torch.cuda.synchronize()
+    pipe.check()
+    for k, (img, lbl) in enumerate(outs):
+        assert torch.equal(img, ref[k % 2][0]) and torch.equal(lbl, ref[k % 2][1])
+    for k in (0, 47):
+        _check(outs[2][0][k].cpu().numpy(), oracle.jpeg_to_tensor(c2[k]), f"pipe[{k}]")
+    bad = ldt_amd.ResidentBatch([c2[0], read_golden("jpeg/bad_truncated.bin")], [0, 1])
+    pipe.decode(bad)
+    with pytest.raises(ldt_amd.ImageDecodeError) as ei:
+        pipe.check()
+    assert ei.value.rows == {1: 3}
+
+
 def test_lance_dataset_end_to_end(tmp_path):
     import ldt_amd
     from ldt_amd import synth
