@@ -99,7 +99,9 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-images", type=int, default=3072)
-    ap.add_argument("--depth", type=int, default=2,
+    ap.add_argument("--no-stage-events", action="store_true",
+                    help="time without the per-stage HIP events (no roofline)")
+    ap.add_argument("--depth", type=int, default=3,
                     help="batches in flight (ldt_amd.DecodePipeline: one context + HIP stream each)")
     args = ap.parse_args()
 
@@ -127,7 +129,7 @@ def main():
     B = args.batch or wl["batch"]
     ctx = _lib.get_context(dev.index)
     ctx.set_option(_lib.OPT_SYNC_STATUS, 0)
-    ctx.set_option(_lib.OPT_PROFILE, 1)
+    ctx.set_option(_lib.OPT_PROFILE, 0 if args.no_stage_events else 1)
 
     cells = None
     if args.workload == "c5":
@@ -151,7 +153,7 @@ def main():
         bytes_per_img = float(np.mean([h * w * 3 for (h, w) in px])) + OUT_BYTES
         comp_bytes = float(np.mean([len(c) for c in cells_all]))
         it = [0]
-        pipe = ldt_amd.DecodePipeline(depth=args.depth, device=dev, profile=True)
+        pipe = ldt_amd.DecodePipeline(depth=args.depth, device=dev, profile=not args.no_stage_events)
 
         def step():
             b = batches[it[0] % nb]

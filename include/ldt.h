@@ -62,6 +62,8 @@ extern "C" {
                                  multiple of 32 (default 1024)                  */
 #define LDT_OPT_PROFILE 4     /* 1: record HIP events around every stage on the
                                  caller's stream (read with ldt_stage_times)    */
+#define LDT_OPT_RESIZE_IMPL 5 /* 0 auto (default): one wave per band; 2: the
+                                 banded workgroup kernel (cross-check)          */
 
 /* ---- stages reported by ldt_stage_times ---- */
 #define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */

@@ -270,8 +270,10 @@ struct ldt_ctx {
   std::string err;
   bool sync_status = true;
   int huff_mode = 0;
+  int resize_impl = 0;
   int subseq_bits = 1024;
-  DevBuf d_data, d_plan, d_dstuf, d_coef, d_planes, d_raw, d_sub, d_pre, d_dscnt;
+  DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_sub, d_pre, d_dscnt;
+  bool coef_dirty = false; // a batch wrote coefficients but k_idct did not run
   static constexpr int kSlots = 2;
   PinBuf h_data[kSlots], h_plan[kSlots];
   hipEvent_t slot_ev[kSlots] = {nullptr, nullptr};
@@ -329,9 +331,10 @@ int set_err(ldt_ctx *c, int code, const char *fmt, ...) {
       return set_err(ctx, LDT_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));         \
   } while (0)
 
-// Grow a device buffer; contents are not preserved. Synchronises `s` first so
-// no in-flight work still references the old allocation.
-int ensure_dev(ldt_ctx *c, DevBuf &b, size_t need, hipStream_t s) {
+// Grow a device buffer; contents are not preserved (a new allocation is
+// zero-filled on `s` when `zero`). Synchronises `s` first so no in-flight work
+// still references the old allocation.
+int ensure_dev(ldt_ctx *c, DevBuf &b, size_t need, hipStream_t s, bool zero = false) {
   if (b.cap >= need) return LDT_OK;
   size_t cap = need + need / 4 + 4096;
   if (b.p) {
@@ -344,6 +347,7 @@ int ensure_dev(ldt_ctx *c, DevBuf &b, size_t need, hipStream_t s) {
   if (hipMalloc(&b.p, cap) != hipSuccess)
     return set_err(c, LDT_ERR_NOMEM, "hipMalloc(%zu) failed", cap);
   b.cap = cap;
+  if (zero) HIPCHK(c, hipMemsetAsync(b.p, 0, cap, s));
   return LDT_OK;
 }
 
@@ -717,7 +721,14 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   // ---- device workspace ----
   if ((rc = ensure_dev(c, c->d_plan, (size_t)plan_bytes, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 64, s))) return rc;
-  if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 130 + 64, s))) return rc;
+  // coefficients: all zero between batches (k_idct clears every block it
+  // reads), so they are zeroed only when allocated
+  if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 128 + 64, s, true))) return rc;
+  if ((rc = ensure_dev(c, c->d_dcv, (size_t)coef_blocks * 2 + 64, s))) return rc;
+  if (c->coef_dirty) {
+    HIPCHK(c, hipMemsetAsync(c->d_coef.p, 0, c->d_coef.cap, s));
+    c->coef_dirty = false;
+  }
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dscnt, 16 * (size_t)(n_chunks + 1), s))) return rc;
   if (parallel && n_wg) {
@@ -739,7 +750,6 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   HIPCHK(c, hipEventRecord(c->slot_ev[sl], s));
   c->slot_used[sl] = true;
   prof_mark(c, LDT_STAGE_H2D, s);
-  if (coef_blocks > 0) HIPCHK(c, hipMemsetAsync(c->d_coef.p, 0, (size_t)coef_blocks * 128, s));
 
   uint8_t *dp = static_cast<uint8_t *>(c->d_plan.p);
   DevPlan p;
@@ -768,7 +778,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.data = dev_cells;
   w.dstuf = static_cast<uint8_t *>(c->d_dstuf.p);
   w.coef = static_cast<int16_t *>(c->d_coef.p);
-  w.dcv = w.coef + coef_blocks * 64;
+  w.dcv = static_cast<int16_t *>(c->d_dcv.p);
   w.planes = static_cast<uint8_t *>(c->d_planes.p);
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
   w.sub = static_cast<SubState *>(c->d_sub.p);
@@ -777,15 +787,19 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
 
   HIPCHK(c, launch_destuff(p, w, s));
   prof_mark(c, LDT_STAGE_DESTUFF, s);
+  c->coef_dirty = true;
   if (parallel) HIPCHK(c, launch_huff_parallel(p, w, s));
   else HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_dc_scan(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
   HIPCHK(c, launch_idct(p, w, s));
+  c->coef_dirty = false;
   prof_mark(c, LDT_STAGE_IDCT, s);
   {
     hipError_t rerr = hipSuccess;
-    if (!launch_resize2_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr))
+    if (!(c->resize_impl != 2 &&
+          launch_resize4_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr)) &&
+        !launch_resize2_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr))
       rerr = launch_resize_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s);
     HIPCHK(c, rerr);
   }
@@ -855,8 +869,8 @@ void ldt_destroy(ldt_ctx *c) {
   if (!c) return;
   DeviceGuard g(c->device);
   (void)hipDeviceSynchronize();
-  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_planes, &c->d_raw,
-                    &c->d_sub, &c->d_pre, &c->d_dscnt};
+  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_dcv,
+                    &c->d_planes, &c->d_raw, &c->d_sub, &c->d_pre, &c->d_dscnt};
   for (DevBuf *b : dbs)
     if (b->p) (void)hipFree(b->p);
   for (int k = 0; k < ldt_ctx::kSlots; ++k) {
@@ -883,6 +897,10 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     return LDT_OK;
   case LDT_OPT_PROFILE:
     c->profile = value != 0;
+    return LDT_OK;
+  case LDT_OPT_RESIZE_IMPL:
+    if (value != 0 && value != 2) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
+    c->resize_impl = (int)value;
     return LDT_OK;
   case LDT_OPT_SUBSEQ_BITS:
     if (value < 64 || value > 2048 || (value & 31))
@@ -995,7 +1013,10 @@ int ldt_resize_raw(ldt_ctx *c, const uint8_t *hwc, int hwc_is_device, int64_t n,
   prof_begin(c, LDT_STAGE_RESIZE, s);
   {
     hipError_t rerr = hipSuccess;
-    if (!launch_resize2_raw(src, cell_stride, (int)n, h, w, static_cast<const float *>(c->d_plan.p),
+    if (!(c->resize_impl != 2 &&
+          launch_resize4_raw(src, cell_stride, (int)n, h, w, static_cast<const float *>(c->d_plan.p),
+                             out_img_dev, s, &rerr)) &&
+        !launch_resize2_raw(src, cell_stride, (int)n, h, w, static_cast<const float *>(c->d_plan.p),
                             out_img_dev, s, &rerr))
       rerr = launch_resize_raw(src, cell_stride, (int)n, h, w,
                                static_cast<const float *>(c->d_plan.p), out_img_dev, s);

@@ -239,7 +239,9 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
 // Coefficient-writing decode of one range: from the reader's position until
 // it reaches `stop` or the segment's `total` blocks are complete. cursor is
 // the current block (segment-relative, -1 before the first DC). DC symbols
-// store their difference in dcv_seg[cursor] (k_dc_scan adds the predictors).
+// store their difference in dcv_seg[cursor] (k_dc_scan adds the predictors);
+// nonzero AC coefficients go to coef_seg, which is all zero beforehand
+// (k_idct clears every block it reads).
 template <class W, class NAT>
 __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
                                           int64_t &cursor, int64_t total,
@@ -863,8 +865,8 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
     const int32_t *__restrict__ wg_img, int S, const SubState *__restrict__ sub,
-    const int32_t *__restrict__ pre, int16_t *__restrict__ coef, int16_t *__restrict__ dcv,
-    int32_t *__restrict__ status) {
+    const int32_t *__restrict__ pre, int16_t *__restrict__ coef,
+    int16_t *__restrict__ dcv, int32_t *__restrict__ status) {
   __shared__ uint8_t s_nat[80];
   __shared__ unsigned long long sh_lohi[2];
   const int img = wg_img[blockIdx.x];
@@ -891,8 +893,8 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
     write_lane(LdsWords{(lds_cu32)win}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv,
                (lds_cu8)s_nat, status, img);
   else
-    write_lane(GlobWords{sc.gw}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv, (lds_cu8)s_nat,
-               status, img);
+    write_lane(GlobWords{sc.gw}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv,
+               (lds_cu8)s_nat, status, img);
 }
 
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {
@@ -908,8 +910,8 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
   hipLaunchKernelGGL(k_huff_scan, dim3(p.n), dim3(256), 0, s, p.descs, p.segs, w.sub, w.sub_pre,
                      w.status);
   hipLaunchKernelGGL(k_huff_write, dim3(p.n_wg), dim3(kSyncThreads), dec_lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.sub_pre, w.coef, w.dcv,
-                     w.status);
+                     p.htabs, w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.sub_pre, w.coef,
+                     w.dcv, w.status);
   return hipGetLastError();
 }
 

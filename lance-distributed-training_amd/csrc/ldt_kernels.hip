@@ -399,101 +399,128 @@ __device__ __forceinline__ Islow8 islow_1d(const int32_t *x, int pass1) {
   return r;
 }
 
-// jdmaster.c prepare_range_limit_table, post-IDCT part, indexed by x & 1023.
+// jdmaster.c prepare_range_limit_table, post-IDCT part, indexed by x & 1023:
+// [0,128) -> x + 128, [128,512) -> 255, [512,896) -> 0, [896,1024) -> x - 896,
+// i.e. clamp(sext10(x) + 128, 0, 255).
 __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
-  int i = x & 1023;
-  return i < 128 ? (uint32_t)(i + 128) : (i < 512 ? 255u : (i < 896 ? 0u : (uint32_t)(i - 896)));
+  const int32_t v = (int32_t)__builtin_amdgcn_sbfe(x, 0u, 10u) + 128;
+  return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
-// One wave handles 8 blocks at a time (lane = row r of block bl), exchanging
-// columns/rows through a wave-private LDS tile: no workgroup barriers. A
-// workgroup (4 waves) covers kIdctBlocksPerWg consecutive blocks of one image.
-constexpr int kIdctBlocksPerWg = 128;
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
+// One lane per 8x8 block: the whole block stays in registers for both
+// passes (no transposes, no barriers between them). A workgroup covers
+// kIdctBlocksPerWg consecutive blocks of one image; their 32 KB of
+// coefficients are read with coalesced 16-byte loads into an LDS tile (block
+// stride 144 B: conflict-free ds_read_b128 per lane), and zeros are written
+// back with the same coalesced stores.
+//
+// Coefficient buffer contract (with k_huff_write): all zero between batches.
+// The Huffman pass writes only nonzero AC coefficients; this kernel clears
+// every block it reads (also for images whose decode failed), so the buffer
+// needs no memset per batch (it is cleared once when allocated).
+constexpr int kIdctBlocksPerWg = 256;
+constexpr int kIdctTileStride = 36; // dwords per block in the LDS tile
 
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
                                               const uint16_t *__restrict__ qtabs,
-                                              const int16_t *__restrict__ coef,
+                                              int16_t *__restrict__ coef,
                                               const int16_t *__restrict__ dcv,
                                               uint8_t *__restrict__ planes,
                                               const int32_t *__restrict__ status) {
-  __shared__ int32_t ws[4][8 * 72];
+  __shared__ __attribute__((aligned(16))) uint32_t s_tile[kIdctBlocksPerWg * kIdctTileStride];
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
   const int img = blockIdx.y;
-  if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const int64_t nblk = (int64_t)d.mcux * d.mcuy * d.bpm;
   const int64_t b0 = (int64_t)blockIdx.x * kIdctBlocksPerWg;
   if (b0 >= nblk) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bl = lane >> 3, r = lane & 7;
-  int32_t *w = &ws[wave][bl * 72];
-  for (int it = 0; it < kIdctBlocksPerWg / 32; ++it) {
-    const int64_t blk = b0 + it * 32 + wave * 8 + bl;
-    const bool valid = blk < nblk;
-    int comp = 0, b = 0;
-    int64_t m = 0;
-    if (valid) {
-      m = blk / d.bpm;
-      b = (int)(blk - m * d.bpm);
-      comp = d.bcomp[b];
-      // row r of the block: 8 int16 = 16 bytes, coalesced across the wave
-      const int4 raw = *reinterpret_cast<const int4 *>(coef + (d.coef_off + blk) * 64 + r * 8);
-      const uint4 q4 = *reinterpret_cast<const uint4 *>(qtabs + d.qt[comp] * 64 + r * 8);
-      const int16_t *cv = reinterpret_cast<const int16_t *>(&raw);
-      const uint16_t *qv = reinterpret_cast<const uint16_t *>(&q4);
-      // DC: absolute value from k_dc_scan (the coefficient slot is unused)
-      const int32_t c0 = r == 0 ? (int32_t)dcv[d.coef_off + blk] : (int32_t)cv[0];
-      w[r * 8] = c0 * (int32_t)qv[0];
+  const int tid = threadIdx.x;
+  const bool ok = status[img] == 0;
+  const int nb = (int)min((int64_t)kIdctBlocksPerWg, nblk - b0);
+  int4 *gsrc = reinterpret_cast<int4 *>(coef + (d.coef_off + b0) * 64);
+  // coalesced: unit u = 16 bytes = row (u & 7) of block (u >> 3)
 #pragma unroll
-      for (int j = 1; j < 8; ++j) w[r * 8 + j] = (int32_t)cv[j] * (int32_t)qv[j];
+  for (int i = 0; i < 8; ++i) {
+    const int u = i * 256 + tid;
+    if ((u >> 3) < nb) {
+      if (ok) {
+        const int4 v = gsrc[u];
+        *reinterpret_cast<int4 *>(&s_tile[(u >> 3) * kIdctTileStride + (u & 7) * 4]) = v;
+      }
+      gsrc[u] = make_int4(0, 0, 0, 0);
     }
-    wave_lds_sync();
-    // pass 1: column r of the block (jidctint.c pass 1, with the DC shortcut)
+  }
+  if (!ok) return; // failed image: only restore the all-zero invariant
+  if (tid < 64 * d.ncomp) s_q[tid >> 6][tid & 63] = qtabs[d.qt[tid >> 6] * 64 + (tid & 63)];
+  __syncthreads();
+  if (tid >= nb) return;
+  const int64_t blk = b0 + tid;
+  const int64_t m = blk / d.bpm;
+  const int b = (int)(blk - m * d.bpm);
+  const int comp = d.bcomp[b];
+  const uint16_t *q = s_q[comp];
+  // dequantised block, row-major (jidctint.c DEQUANTIZE)
+  int32_t ws[64];
+  const uint32_t *tl = &s_tile[tid * kIdctTileStride];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint4 raw = *reinterpret_cast<const uint4 *>(tl + 4 * r);
+    const uint4 q4 = *reinterpret_cast<const uint4 *>(q + 8 * r);
+    const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+    const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int32_t lo = (int32_t)(int16_t)(rw[j] & 0xFFFF), hi = (int32_t)(int16_t)(rw[j] >> 16);
+      ws[8 * r + 2 * j] = lo * (int32_t)(qw[j] & 0xFFFF);
+      ws[8 * r + 2 * j + 1] = hi * (int32_t)(qw[j] >> 16);
+    }
+  }
+  ws[0] = (int32_t)dcv[d.coef_off + blk] * (int32_t)q[0]; // DC: absolute value from k_dc_scan
+  // pass 1: columns (CONST_BITS 13, PASS1_BITS 2). A column whose AC terms are
+  // all zero gives DC << 2 exactly (jidctint.c shortcut); the butterfly runs
+  // when any lane of the wave needs it.
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const bool nz = (ws[8 + c] | ws[16 + c] | ws[24 + c] | ws[32 + c] | ws[40 + c] | ws[48 + c] |
+                     ws[56 + c]) != 0;
+    if (__any(nz)) {
+      int32_t x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = ws[8 * j + c];
+      const Islow8 t = islow_1d(x, 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ws[8 * j + c] = (t.o[j] + (1 << 10)) >> 11; // DESCALE(, 13-2)
+    } else {
+      const int32_t dc4 = ws[c] * 4;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ws[8 * j + c] = dc4;
+    }
+  }
+  // pass 2: rows, DESCALE(, 13+2+3) and the range limit
+  const int mx = (int)(m % d.mcux), my = (int)(m / d.mcux);
+  const int bx = mx * d.ch[comp] + d.bdx[b];
+  const int by = my * d.cv[comp] + d.bdy[b];
+  uint8_t *dst = planes + d.plane_off[comp] + (int64_t)(by * 8) * d.plane_stride[comp] + bx * 8;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
     int32_t x[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = w[j * 8 + r];
-    int32_t o[8];
-    if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = x[0] * (1 << 2);
-    } else {
-      Islow8 t = islow_1d(x, 1);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (t.o[j] + (1 << 10)) >> 11; // DESCALE(, 13-2)
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) w[j * 8 + r] = o[j];
-    wave_lds_sync();
-    // pass 2: row r
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = w[r * 8 + j];
+    for (int j = 0; j < 8; ++j) x[j] = ws[8 * r + j];
+    const bool nz = (x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) != 0;
     uint32_t px[8];
-    if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
+    if (__any(nz)) {
+      const Islow8 t = islow_1d(x, 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) px[j] = idct_limit((t.o[j] + (1 << 17)) >> 18);
+    } else {
       const uint32_t v = idct_limit((x[0] + (1 << 4)) >> 5); // DESCALE(, PASS1_BITS+3)
 #pragma unroll
       for (int j = 0; j < 8; ++j) px[j] = v;
-    } else {
-      Islow8 t = islow_1d(x, 0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) px[j] = idct_limit((t.o[j] + (1 << 17)) >> 18); // DESCALE(, 13+2+3)
     }
-    if (valid) {
-      const int mx = (int)(m % d.mcux), my = (int)(m / d.mcux);
-      const int bx = mx * d.ch[comp] + d.bdx[b];
-      const int by = my * d.cv[comp] + d.bdy[b];
-      uint8_t *dstp = planes + d.plane_off[comp] + (int64_t)(by * 8 + r) * d.plane_stride[comp] + bx * 8;
-      uint2 packed;
-      packed.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
-      packed.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
-      *reinterpret_cast<uint2 *>(dstp) = packed;
-    }
-    wave_lds_sync(); // the tile is rewritten by the next group
+    uint2 packed;
+    packed.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+    packed.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
+    *reinterpret_cast<uint2 *>(dst + (int64_t)r * d.plane_stride[comp]) = packed;
   }
 }
 

@@ -43,7 +43,8 @@ struct DevPlan {
 struct DevWork {
   const uint8_t *data;  // compressed cells
   uint8_t *dstuf;       // destuffed entropy data
-  int16_t *coef;        // coefficients (the DC slot of each block is unused)
+  int16_t *coef;        // AC coefficients (the DC slot of each block is unused); all zero
+                        // between batches (k_idct clears every block it reads)
   int16_t *dcv;         // per block: DC difference (Huffman), then absolute DC (k_dc_scan)
   uint8_t *planes;      // component planes
   int32_t *status;      // per image
@@ -64,6 +65,12 @@ hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, in
 bool launch_resize2_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
                          hipStream_t s, hipError_t *err);
 bool launch_resize2_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int wd,
+                        const float *lut, float *out, hipStream_t s, hipError_t *err);
+// One-wave-per-band resize (ldt_resize4.hip); false when unsupported (wide
+// taps or LDS), then the banded kernel above is used.
+bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
+                         hipStream_t s, hipError_t *err);
+bool launch_resize4_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int wd,
                         const float *lut, float *out, hipStream_t s, hipError_t *err);
 hipError_t launch_resize_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int w,
                              const float *lut, float *out, hipStream_t s);

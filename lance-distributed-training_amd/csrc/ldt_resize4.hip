@@ -1,0 +1,536 @@
+// ldt_resize4.hip — fused source staging + Pillow BILINEAR Resize((224,224)) +
+// ToTensor/Normalize store, one wavefront per band of output rows.
+//
+// Every wave owns one (image, band) task and runs it alone: it streams the
+// band's source rows two at a time, stages them as RGBx dwords in a
+// wave-private LDS buffer (raw HWC bytes, or JPEG planes with libjpeg's h2v2
+// fancy upsampling and YCbCr->RGB done in registers), computes the rows'
+// 224x3 horizontal taps (Pillow Resample.c, 22-bit fixed point, clip8) into a
+// wave-private LDS ring of uint8 rows, and finishes every output row whose
+// vertical window is complete: vertical taps, clip8, the ToTensor[/Normalize]
+// float32 LUT and float4 stores into the CHW fp32 output. There is no
+// workgroup barrier after the prologue, so the waves of a CU overlap their
+// loads and arithmetic freely; the next row pair is prefetched into registers
+// while the current one is computed.
+//
+// Reference semantics: lance_iterable.py:28-32 (Resize((224,224)), ToTensor),
+// :31 (Normalize); jdsample.c h2v2_fancy_upsample, jdcolor.c ycc_rgb_convert,
+// Pillow Resample.c ImagingResample (horizontal pass first, uint8 between).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ldt_device.hpp"
+#include "ldt_kernels.hpp"
+
+namespace ldt {
+
+namespace {
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Lane l receives lane l-1's value (lane 0 keeps its own): DPP wave_shr:1.
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);
+}
+// Lane l receives lane l+1's value (lane 63 keeps its own): DPP wave_shl:1.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x130, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ uint32_t rgbx(int r, int g, int b) {
+  return (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
+}
+
+// jdcolor.c ycc_rgb_convert (16-bit fixed point, ONE_HALF in the Cb->G term).
+__device__ __forceinline__ uint32_t ycc_px(int y, int cb, int cr) {
+  const int xcr = cr - 128, xcb = cb - 128;
+  const int r = y + ((91881 * xcr + 32768) >> 16);
+  const int g = y + ((-22554 * xcb + 32768 + (-46802) * xcr) >> 16);
+  const int b = y + ((116130 * xcb + 32768) >> 16);
+  return rgbx(clampi(r, 0, 255), clampi(g, 0, 255), clampi(b, 0, 255));
+}
+
+struct Raw16 {
+  uint4 a, b, c;
+};
+
+__device__ __forceinline__ Raw16 load16_aligned(const uint8_t *p) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  Raw16 r;
+  r.a = q[0];
+  r.b = q[1];
+  r.c = q[2];
+  return r;
+}
+
+// Bytes [3*x0, 3*x0 + 48) of a row, any alignment, zero past the row end.
+__device__ __forceinline__ Raw16 load16_any(const uint8_t *row, int W, int x0) {
+  const uint8_t *p = row + 3 * x0;
+  uint32_t w[12];
+  const int nb = max(0, min(48, 3 * (W - x0)));
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (4 * i + e < nb) v |= (uint32_t)p[4 * i + e] << (8 * e);
+    w[i] = v;
+  }
+  Raw16 r;
+  r.a = make_uint4(w[0], w[1], w[2], w[3]);
+  r.b = make_uint4(w[4], w[5], w[6], w[7]);
+  r.c = make_uint4(w[8], w[9], w[10], w[11]);
+  return r;
+}
+
+// 16 packed RGB pixels -> 16 RGBx dwords at row[x0..x0+16). The byte above B
+// is left as whatever follows (the taps read bytes 0..2 only).
+__device__ __forceinline__ void stage16_raw(const Raw16 &r, uint32_t *row, int x0) {
+  const uint32_t w[13] = {r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w,
+                          r.c.x, r.c.y, r.c.z, r.c.w, 0u};
+  uint32_t px[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int o = 3 * j;
+    px[j] = __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], (uint32_t)(o & 3));
+  }
+  uint4 *d = reinterpret_cast<uint4 *>(row + x0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) d[q] = make_uint4(px[4 * q], px[4 * q + 1], px[4 * q + 2], px[4 * q + 3]);
+}
+
+// One JPEG row pair's registers for the 4:2:0 fast path (lane = 8 pixels).
+struct Jpair {
+  uint2 y0, y1;        // luma rows 2cy, 2cy+1 (8 px each)
+  uint32_t c[2][3];    // chroma comp (Cb, Cr) x row (cy-1, cy, cy+1), 4 samples each
+};
+
+__device__ __forceinline__ void bytes6(uint32_t w, int lane, int rc, int s[6]) {
+  const uint32_t p = from_prev_lane(w), n = from_next_lane(w);
+  s[0] = (int)(p >> 24);
+  s[1] = (int)(w & 255);
+  s[2] = (int)((w >> 8) & 255);
+  s[3] = (int)((w >> 16) & 255);
+  s[4] = (int)(w >> 24);
+  s[5] = (int)(n & 255);
+  // column -1 -> column 0; columns past downsampled_width - 1 -> that column
+  // (jdsample.c special first/last columns, context rows replicated)
+  s[0] = lane == 0 ? s[1] : s[0];
+  int e = s[1];
+#pragma unroll
+  for (int i = 2; i <= 5; ++i) e = rc == i ? s[i] : e;
+#pragma unroll
+  for (int i = 2; i <= 5; ++i) s[i] = i > rc ? e : s[i];
+}
+
+} // namespace
+
+struct Geom4 {
+  int nbands, bh;  // bands per image, output rows per band
+  int ring;        // intermediate ring rows (>= ks_v + 3)
+  int ks_v;        // vertical taps (max over the batch)
+  int spad;        // staging row stride in dwords (multiple of 4)
+  int ntask;       // n * nbands
+  int wave_bytes;  // LDS per wave
+};
+
+constexpr int kKvRows = 16; // vertical coefficient rows cached per wave
+
+template <int SRC, int KS>
+__global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ descs,
+                                                 const uint8_t *__restrict__ planes, RawSrc raw,
+                                                 const float *__restrict__ lut,
+                                                 const int64_t *__restrict__ labels,
+                                                 float *__restrict__ out,
+                                                 int64_t *__restrict__ out_labels,
+                                                 const int32_t *__restrict__ status, Geom4 g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float *s_lut = reinterpret_cast<float *>(smem);
+  for (int i = tid; i < 768; i += 256) s_lut[i] = lut[i];
+  __syncthreads(); // the only workgroup barrier
+  const int task = blockIdx.x * 4 + wave;
+  if (task >= g.ntask) return;
+  const int img = task / g.nbands, band = task - img * g.nbands;
+  if (SRC == 0 && status[img] != 0) return;
+  int W, H;
+  if constexpr (SRC == 0) {
+    W = descs[img].width;
+    H = descs[img].height;
+  } else {
+    W = raw.w;
+    H = raw.h;
+  }
+  const int oy0 = band * g.bh;
+  const int nb = min(g.bh, kOut - oy0);
+  if (nb <= 0) return;
+  if (band == 0 && lane == 0 && labels != nullptr) out_labels[img] = labels[img];
+
+  uint8_t *wbase = smem + 3072 + wave * g.wave_bytes;
+  uint32_t *stg = reinterpret_cast<uint32_t *>(wbase);               // 2 * spad dwords
+  uint8_t *ring = wbase + 8 * g.spad;                                // 3 * ring * 224
+  int32_t *kv = reinterpret_cast<int32_t *>(ring + 3 * g.ring * kOut); // kKvRows * ks_v
+  int32_t *vb = kv + kKvRows * g.ks_v;                               // kKvRows * 2
+  const int ks_v = g.ks_v, RING = g.ring;
+
+  // horizontal weights of this lane's output columns, in registers:
+  // q = 0..2 -> column lane + 64q of both rows; q = 3 -> column 192 + lane%32
+  // of row (lane / 32)
+  int32_t wgt[4][KS];
+  int xm[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int ox = q < 3 ? lane + 64 * q : 192 + (lane & 31);
+    int32_t k[KS];
+    resample_coeffs_one(W, kOut, ox, KS, k, &xm[q]);
+#pragma unroll
+    for (int t = 0; t < KS; ++t) wgt[q][t] = k[t];
+  }
+  // band source rows
+  int ya, yb;
+  {
+    int32_t kk[32];
+    int ymin_a, ymin_b;
+    resample_coeffs_one(H, kOut, oy0, 0, kk, &ymin_a);
+    const int cnt_b = resample_coeffs_one(H, kOut, oy0 + nb - 1, 0, kk, &ymin_b);
+    ya = ymin_a;
+    yb = ymin_b + cnt_b;
+  }
+  const int ya0 = SRC == 0 ? (ya & ~1) : ya;
+
+  // vertical-pass items: 168 dwords (3 channels x 56 groups of 4 columns)
+  int vc[3], vo[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int it = min(lane + 64 * i, 167);
+    vc[i] = it / 56;
+    vo[i] = (it - vc[i] * 56) * 4;
+  }
+
+  // JPEG fast path: 4:2:0 with both chroma planes fancy-upsampled, W <= 512
+  bool fast420 = false;
+  int rc = 5, cdh = 1;
+  const ImgDesc *dp = nullptr;
+  const uint8_t *raw_cell = nullptr;
+  bool raw_al16 = false;
+  if constexpr (SRC == 0) {
+    dp = descs + img;
+    const ImgDesc &d = *dp;
+    fast420 = d.color == 0 && d.hf[1] == 2 && d.vf[1] == 2 && d.hf[2] == 2 && d.vf[2] == 2 &&
+              d.cdw[1] > 2 && d.cdw[2] > 2 && d.cdw[1] == d.cdw[2] && d.cdh[1] == d.cdh[2] &&
+              d.plane_stride[1] == d.plane_stride[2] && W <= 512;
+    const int dw = d.cdw[1];
+    rc = lane == (dw - 1) / 4 ? (dw - 1) % 4 + 1 : 5;
+    cdh = d.cdh[1];
+  } else {
+    raw_cell = raw.base + (int64_t)img * raw.cell_stride;
+    raw_al16 = ((((uintptr_t)raw_cell) & 15) == 0) && ((W * 3) & 15) == 0 && W <= 1024;
+  }
+
+  // ---- prefetch helpers ----
+  Jpair jp;
+  Raw16 rp0, rp1;
+  auto fetch = [&](int y) {
+    if constexpr (SRC == 0) {
+      if (fast420) {
+        const ImgDesc &d = *dp;
+        const int x0 = lane * 8;
+        const uint8_t *py = planes + d.plane_off[0] + (int64_t)y * d.plane_stride[0] + x0;
+        jp.y0 = x0 < W ? *reinterpret_cast<const uint2 *>(py) : make_uint2(0, 0);
+        jp.y1 = (x0 < W && y + 1 < H) ? *reinterpret_cast<const uint2 *>(py + d.plane_stride[0])
+                                     : make_uint2(0, 0);
+        const int cy = y >> 1;
+        const int rows[3] = {max(cy - 1, 0), cy, min(cy + 1, cdh - 1)};
+        const int cx0 = lane * 4;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+            jp.c[c][r] = cx0 < d.plane_stride[1]
+                             ? *reinterpret_cast<const uint32_t *>(planes + d.plane_off[1 + c] +
+                                                                   (int64_t)rows[r] * d.plane_stride[1] + cx0)
+                             : 0u;
+      }
+    } else {
+      if (raw_al16) {
+        const int x0 = lane * 16;
+        if (x0 < W) {
+          rp0 = load16_aligned(raw_cell + (int64_t)y * W * 3 + 3 * x0);
+          if (y + 1 < H) rp1 = load16_aligned(raw_cell + (int64_t)(y + 1) * W * 3 + 3 * x0);
+        }
+      }
+    }
+  };
+
+  // ---- staging of one row pair into stg[0..spad) / stg[spad..2 spad) ----
+  auto stage = [&](int y) {
+    uint32_t *s0 = stg, *s1 = stg + g.spad;
+    if constexpr (SRC == 0) {
+      const ImgDesc &d = *dp;
+      if (fast420) {
+        const int x0 = lane * 8;
+        int cb[2][8], crr[2][8];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          int A[6], U[6], D[6];
+          bytes6(jp.c[c][1], lane, rc, A);
+          bytes6(jp.c[c][0], lane, rc, U);
+          bytes6(jp.c[c][2], lane, rc, D);
+          int T[6], B[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            T[i] = A[i] * 3 + U[i];
+            B[i] = A[i] * 3 + D[i];
+          }
+          int *o0 = c == 0 ? cb[0] : crr[0];
+          int *o1 = c == 0 ? cb[1] : crr[1];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int ci = (j >> 1) + 1;
+            const int nt = (j & 1) ? T[ci + 1] : T[ci - 1];
+            const int nbv = (j & 1) ? B[ci + 1] : B[ci - 1];
+            o0[j] = (T[ci] * 3 + nt + 8 - (j & 1)) >> 4;
+            o1[j] = (B[ci] * 3 + nbv + 8 - (j & 1)) >> 4;
+          }
+        }
+        uint32_t p0[8], p1[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t ya_ = j < 4 ? jp.y0.x : jp.y0.y, yb_ = j < 4 ? jp.y1.x : jp.y1.y;
+          const int sh = 8 * (j & 3);
+          p0[j] = ycc_px((int)((ya_ >> sh) & 255), cb[0][j], crr[0][j]);
+          p1[j] = ycc_px((int)((yb_ >> sh) & 255), cb[1][j], crr[1][j]);
+        }
+        if (x0 < W) {
+          uint4 *d0 = reinterpret_cast<uint4 *>(s0 + x0);
+          uint4 *d1 = reinterpret_cast<uint4 *>(s1 + x0);
+          d0[0] = make_uint4(p0[0], p0[1], p0[2], p0[3]);
+          d0[1] = make_uint4(p0[4], p0[5], p0[6], p0[7]);
+          d1[0] = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+          d1[1] = make_uint4(p1[4], p1[5], p1[6], p1[7]);
+        }
+      } else {
+        // generic: any supported sampling, gray, RGB, wide images
+        const uint8_t *pl0 = planes + d.plane_off[0];
+        for (int r = 0; r < 2; ++r) {
+          const int yy = y + r;
+          if (yy >= H) break;
+          uint32_t *sr = r ? s1 : s0;
+          for (int x0 = lane * 8; x0 < W; x0 += 512) {
+            uint32_t px[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int x = min(x0 + j, W - 1);
+              const int Y = pl0[(int64_t)yy * d.plane_stride[0] + x];
+              if (d.color == 2) {
+                px[j] = rgbx(Y, Y, Y);
+              } else {
+                const int cb = chroma_at(d, planes + d.plane_off[1], 1, x, yy);
+                const int cr = chroma_at(d, planes + d.plane_off[2], 2, x, yy);
+                px[j] = d.color == 1 ? rgbx(Y, cb, cr) : ycc_px(Y, cb, cr);
+              }
+            }
+            uint4 *dd = reinterpret_cast<uint4 *>(sr + x0);
+            dd[0] = make_uint4(px[0], px[1], px[2], px[3]);
+            dd[1] = make_uint4(px[4], px[5], px[6], px[7]);
+          }
+        }
+      }
+    } else {
+      if (raw_al16) {
+        if (lane * 16 < W) {
+          stage16_raw(rp0, s0, lane * 16);
+          if (y + 1 < H) stage16_raw(rp1, s1, lane * 16);
+        }
+      } else {
+        for (int r = 0; r < 2; ++r) {
+          const int yy = y + r;
+          if (yy >= H) break;
+          const uint8_t *row = raw_cell + (int64_t)yy * W * 3;
+          for (int x0 = lane * 16; x0 < W; x0 += 1024) stage16_raw(load16_any(row, W, x0), r ? s1 : s0, x0);
+        }
+      }
+    }
+  };
+
+  int next_oy = 0;     // next output row of the band to finish
+  int kv_base = -1;    // first band row cached in kv
+  int slot = 0;        // ring slot of row y
+  fetch(ya0);
+  for (int y = ya0; y < yb; y += 2) {
+    stage(y);
+    if (y + 2 < yb) fetch(y + 2);
+    wave_lds_fence();
+    // horizontal taps: 7 (q, row) jobs of 64 output columns
+    const int slot1 = slot + 1 == RING ? 0 : slot + 1;
+#pragma unroll
+    for (int job = 0; job < 7; ++job) {
+      const int q = job < 6 ? job >> 1 : 3;
+      const int r = job < 6 ? (job & 1) : (lane >> 5);
+      const int ox = q < 3 ? lane + 64 * q : 192 + (lane & 31);
+      const uint32_t *src = stg + (r ? g.spad : 0) + xm[q];
+      int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        const uint32_t v = src[t];
+        const int32_t kw = wgt[q][t];
+        a0 += (int32_t)(v & 255) * kw;
+        a1 += (int32_t)((v >> 8) & 255) * kw;
+        a2 += (int32_t)((v >> 16) & 255) * kw;
+      }
+      const int sl = r ? slot1 : slot;
+      uint8_t *rw = ring + sl * kOut + ox;
+      rw[0] = (uint8_t)min((uint32_t)a0 >> kPrecisionBits, 255u);
+      rw[RING * kOut] = (uint8_t)min((uint32_t)a1 >> kPrecisionBits, 255u);
+      rw[2 * RING * kOut] = (uint8_t)min((uint32_t)a2 >> kPrecisionBits, 255u);
+    }
+    slot = slot1 + 1 == RING ? 0 : slot1 + 1;
+    wave_lds_fence();
+    // finish every output row whose vertical window is complete
+    const int done = y + 2; // rows [ya0, done) are in the ring
+    while (next_oy < nb) {
+      const int j = next_oy;
+      if (j >= kv_base + kKvRows || kv_base < 0) {
+        kv_base = j;
+        if (lane < kKvRows && j + lane < nb) {
+          int ymin;
+          const int cnt = resample_coeffs_one(H, kOut, oy0 + j + lane, ks_v, kv + lane * ks_v, &ymin);
+          vb[2 * lane] = ymin;
+          vb[2 * lane + 1] = cnt;
+        }
+        wave_lds_fence();
+      }
+      const int jr = j - kv_base;
+      const int ymin = __builtin_amdgcn_readfirstlane(vb[2 * jr]);
+      const int cnt = __builtin_amdgcn_readfirstlane(vb[2 * jr + 1]);
+      if (ymin + cnt > done) break;
+      ++next_oy;
+      int s0 = (ymin - ya0) % RING;
+      int32_t acc[3][4];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][e] = 1 << (kPrecisionBits - 1);
+      for (int t = 0; t < cnt; ++t) {
+        const int32_t kw = __builtin_amdgcn_readfirstlane(kv[jr * ks_v + t]);
+        const int sl = s0 + t < RING ? s0 + t : s0 + t - RING;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const uint32_t v = *reinterpret_cast<const uint32_t *>(ring + (vc[i] * RING + sl) * kOut + vo[i]);
+          acc[i][0] += (int32_t)(v & 255) * kw;
+          acc[i][1] += (int32_t)((v >> 8) & 255) * kw;
+          acc[i][2] += (int32_t)((v >> 16) & 255) * kw;
+          acc[i][3] += (int32_t)(v >> 24) * kw;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (lane + 64 * i < 168) {
+          const float *lc = s_lut + vc[i] * 256;
+          float4 f;
+          f.x = lc[min((uint32_t)acc[i][0] >> kPrecisionBits, 255u)];
+          f.y = lc[min((uint32_t)acc[i][1] >> kPrecisionBits, 255u)];
+          f.z = lc[min((uint32_t)acc[i][2] >> kPrecisionBits, 255u)];
+          f.w = lc[min((uint32_t)acc[i][3] >> kPrecisionBits, 255u)];
+          *reinterpret_cast<float4 *>(out + (((int64_t)img * 3 + vc[i]) * kOut + oy0 + j) * kOut + vo[i]) = f;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launch geometry.
+// ---------------------------------------------------------------------------
+static int wave_bytes4(const Geom4 &g) {
+  const int b = 8 * g.spad + 3 * g.ring * kOut + 4 * (kKvRows * g.ks_v + 2 * kKvRows);
+  return (b + 15) & ~15;
+}
+
+static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g) {
+  g.ks_v = resample_ksize_host(max_h, kOut);
+  g.ring = g.ks_v + 3;
+  g.spad = ((((max_w + 15) / 16) * 16 + ks_h + 16) + 3) & ~3;
+  g.wave_bytes = wave_bytes4(g);
+  int nb = (waves_target + n - 1) / n;
+  if (nb < 1) nb = 1;
+  if (nb > 28) nb = 28;
+  g.bh = (kOut + nb - 1) / nb;
+  g.nbands = (kOut + g.bh - 1) / g.bh;
+  g.ntask = n * g.nbands;
+  return 3072 + 4 * (size_t)g.wave_bytes <= 160 * 1024;
+}
+
+template <int SRC, int KS>
+static hipError_t launch4(const ImgDesc *descs, const uint8_t *planes, RawSrc raw, const float *lut,
+                          const int64_t *labels, float *out, int64_t *out_labels,
+                          const int32_t *status, const Geom4 &g, hipStream_t s) {
+  static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resize4<SRC, KS>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  const int groups = (g.ntask + 3) / 4;
+  hipLaunchKernelGGL((k_resize4<SRC, KS>), dim3(groups), dim3(256), 3072 + 4 * g.wave_bytes, s, descs,
+                     planes, raw, lut, labels, out, out_labels, status, g);
+  return hipGetLastError();
+}
+
+template <int SRC>
+static bool dispatch4(int ks_h, const ImgDesc *descs, const uint8_t *planes, RawSrc raw,
+                      const float *lut, const int64_t *labels, float *out, int64_t *out_labels,
+                      const int32_t *status, const Geom4 &g, hipStream_t s, hipError_t *err) {
+  switch (ks_h) {
+  case 3: *err = launch4<SRC, 3>(descs, planes, raw, lut, labels, out, out_labels, status, g, s); return true;
+  case 5: *err = launch4<SRC, 5>(descs, planes, raw, lut, labels, out, out_labels, status, g, s); return true;
+  case 7: *err = launch4<SRC, 7>(descs, planes, raw, lut, labels, out, out_labels, status, g, s); return true;
+  case 9: *err = launch4<SRC, 9>(descs, planes, raw, lut, labels, out, out_labels, status, g, s); return true;
+  case 11: *err = launch4<SRC, 11>(descs, planes, raw, lut, labels, out, out_labels, status, g, s); return true;
+  default: return false;
+  }
+}
+
+// Waves to aim for: the CU count times the resident waves per CU the LDS
+// allows (at most 12).
+static int waves_target4(const Geom4 &g) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) cus = 256;
+    else cus = prop.multiProcessorCount;
+  }
+  int wg = (160 * 1024) / (3072 + 4 * g.wave_bytes);
+  if (wg > 3) wg = 3;
+  if (wg < 1) wg = 1;
+  return cus * 4 * wg;
+}
+
+bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
+                         hipStream_t s, hipError_t *err) {
+  Geom4 g;
+  const int ks_h = resample_ksize_host(p.max_w, kOut);
+  if (ks_h > 11) return false;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g)) return false;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g), g)) return false;
+  RawSrc raw{nullptr, 0, 0, 0};
+  return dispatch4<0>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s,
+                      err);
+}
+
+bool launch_resize4_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int wd,
+                        const float *lut, float *out, hipStream_t s, hipError_t *err) {
+  Geom4 g;
+  const int ks_h = resample_ksize_host(wd, kOut);
+  if (ks_h > 11) return false;
+  if (!make_geom4(n, wd, h, ks_h, 1, g)) return false;
+  if (!make_geom4(n, wd, h, ks_h, waves_target4(g), g)) return false;
+  RawSrc raw{hwc, cell_stride, h, wd};
+  return dispatch4<1>(ks_h, (const ImgDesc *)nullptr, (const uint8_t *)nullptr, raw, lut,
+                      (const int64_t *)nullptr, out, (int64_t *)nullptr, (const int32_t *)nullptr, g,
+                      s, err);
+}
+
+} // namespace ldt

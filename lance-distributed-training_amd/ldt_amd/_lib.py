@@ -41,6 +41,7 @@ OPT_SYNC_STATUS = 1
 OPT_HUFF_MODE = 2
 OPT_SUBSEQ_BITS = 3
 OPT_PROFILE = 4
+OPT_RESIZE_IMPL = 5
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
 

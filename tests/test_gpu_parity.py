@@ -331,3 +331,43 @@ def test_tall_bands_large_batches():
     img = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
     for k in (0, 3, 201, 399):
         _check(img[k], oracle.jpeg_to_tensor(cells[k]), f"jpeg400[{k}]")
+
+
+def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
+    """The one-wave-per-band resize (default) and the banded workgroup kernel
+    (LDT_OPT_RESIZE_IMPL=2) give identical tensors on every golden image and on
+    unaligned raw cells; a batch with a truncated image leaves no coefficient
+    residue for the next batch (k_idct clears what the Huffman pass wrote)."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    ctx = _lib.get_context(0)
+    ents = manifest["images"]
+    cells = [read_golden(e["file"]) for e in ents]
+    raw = synth.raw_hwc(3, 301, 517, seed=5)  # 517*3 bytes per row: unaligned rows
+    flat = np.concatenate([np.zeros(5, np.uint8), raw.reshape(-1)])
+    arr = pa.array([flat[5 + k * raw[0].size: 5 + (k + 1) * raw[0].size].tobytes() for k in range(3)],
+                   type=pa.binary(raw[0].size))
+    res = {}
+    try:
+        for impl in (0, 2):
+            ctx.set_option(_lib.OPT_RESIZE_IMPL, impl)
+            a = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+            b = ldt_amd.resize_raw(arr, 301, 517, normalize=True).cpu().numpy()
+            res[impl] = (a, b)
+    finally:
+        ctx.set_option(_lib.OPT_RESIZE_IMPL, 0)
+    assert np.array_equal(res[0][0], res[2][0])
+    assert np.array_equal(res[0][1], res[2][1])
+    for k in range(3):
+        _check(res[0][1][k], oracle.raw_to_tensor(raw[k], normalize=True), f"raw301x517[{k}]")
+    good = synth.encode(synth.field(384, 512, 11), quality=90)
+    bad = read_golden("jpeg/bad_truncated.bin")
+    with pytest.raises(ldt_amd.ImageDecodeError):
+        ldt_amd.decode_tensor_image(_batch([good, bad, good]))
+    nxt = [synth.encode(synth.field(512, 384, 12 + i)) for i in range(3)]
+    img = ldt_amd.decode_tensor_image(_batch(nxt))["image"].cpu().numpy()
+    for k in range(3):
+        _check(img[k], oracle.jpeg_to_tensor(nxt[k]), f"after-error[{k}]")
