@@ -186,6 +186,20 @@ def main():
     total_imgs = B * args.steps * world
     value = total_imgs / elapsed_max
 
+    # standalone launch durations (one batch in flight, after the timed region)
+    standalone = None
+    if args.workload != "c5" and not args.no_stage_events:
+        solo = ldt_amd.DecodePipeline(depth=1, device=dev, profile=True)
+        for k in range(2):
+            solo.decode(batches[k % nb])
+        barrier()
+        solo.stage_times(reset=True)
+        for k in range(4):
+            solo.decode(batches[k % nb])
+        barrier()
+        standalone = solo.stage_times(reset=True)
+        solo.check()
+
     # roofline: the resize/normalise stage (north_star), from live HIP events
     rs_ms, rs_n = stages["resize"]
     rs_avg_s = rs_ms / max(rs_n, 1) / 1e3
@@ -224,6 +238,24 @@ def main():
         "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items()},
         "dominant_stage": dominant,
     }
+    if standalone is not None:
+        sa_ms, sa_n = standalone["resize"]
+        sa_s = sa_ms / max(sa_n, 1) / 1e3
+        sa_ach = bytes_per_img * B / sa_s / 1e9 if sa_s > 0 else 0.0
+        res["roofline"]["standalone"] = {
+            "avg_launch_ms": round(sa_s * 1e3, 4), "achieved": round(sa_ach, 1),
+            "frac": round(sa_ach / HBM_PEAK_GBS, 4),
+            "timing": "HIP events, one batch in flight (4 batches after the timed region)"}
+        res["stages_standalone_ms"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in standalone.items()}
+    tr = load_profile(f"traffic_{args.workload}.json")
+    if tr is not None and tr.get("batch", B) == B:
+        res["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+        res["roofline"]["traffic_source"] = (f"profiles/{PROFILE_ROUND}/traffic_{args.workload}.json: rocprofv3 "
+                                             "--pmc FETCH_SIZE and WRITE_SIZE passes (FETCH_SIZE x2, gfx950) "
+                                             "over this bench at depth 1")
+    dec = load_profile(f"pmc_{args.workload}_decode.json")
+    if dec is not None:
+        res["decode_efficiency"] = dec
     if args.workload != "c5":
         res["config"]["compressed_bytes_per_img"] = round(comp_bytes, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "c5":
@@ -236,6 +268,18 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+PROFILE_ROUND = "r1"
+
+
+def load_profile(name: str):
+    """A committed PMC summary under profiles/<round>/ (None if absent)."""
+    path = os.path.join(REPO, "profiles", PROFILE_ROUND, name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
 
 
 def ldt_amd_dims(cell: bytes):

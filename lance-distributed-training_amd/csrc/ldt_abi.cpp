@@ -639,8 +639,20 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     d.src_off = ip.cell_off + H.scan_pos;
     d.src_len = ip.cell_len - H.scan_pos;
     if (parallel) {
+      // subsequence length of this image: without restart markers, the largest
+      // S <= the context's S that still fills its last workgroup (fewer,
+      // fuller workgroups; S stays within the LDS window sized for SB)
+      int64_t sbits = SB;
+      if (d.nseg == 1 && SB >= 256) {
+        const int64_t bits = d.src_len * 8;
+        const int64_t k = std::max<int64_t>(1, (bits + (int64_t)SB * (kSlotsPerWg - 1) - 1) /
+                                                   ((int64_t)SB * (kSlotsPerWg - 1)));
+        sbits = (bits + k * (kSlotsPerWg - 1) - 1) / (k * (kSlotsPerWg - 1));
+        sbits = std::min<int64_t>(SB, std::max<int64_t>(256, (sbits + 31) & ~(int64_t)31));
+      }
+      d.sub_bits = (int32_t)sbits;
       // subsequence slots: sum over segments of ceil(bits_s / S) <= bits / S + nseg
-      const int64_t slots = (d.src_len * 8 + SB - 1) / SB + d.nseg;
+      const int64_t slots = (d.src_len * 8 + sbits - 1) / sbits + d.nseg;
       d.wg_count = (int32_t)((slots + kSlotsPerWg - 1) / kSlotsPerWg);
       d.wg_first = n_wg;
       d.sub_cap = d.wg_count * kSlotsPerWg;

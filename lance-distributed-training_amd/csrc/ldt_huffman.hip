@@ -477,7 +477,7 @@ struct SubCtx {
 // Workgroup setup shared by the sync and write kernels: the image's tables
 // and the LDS window.
 __device__ __forceinline__ Dec sub_setup(const ImgDesc &d, const Segment *__restrict__ segs,
-                                         const HuffTab *__restrict__ htabs, int S,
+                                         const HuffTab *__restrict__ htabs, int S, int Smax,
                                          const uint8_t *__restrict__ dstuf, lds_u32 win,
                                          lds_u16 tabs, unsigned long long *sh_lohi, SubCtx &sc) {
   const int tid = threadIdx.x;
@@ -530,7 +530,7 @@ __device__ __forceinline__ Dec sub_setup(const ImgDesc &d, const Segment *__rest
     wb = (int64_t)sh_lohi[0] & ~(int64_t)3;
     nbytes = (((int64_t)sh_lohi[1] - wb) + 3) & ~(int64_t)3;
   }
-  sc.in_lds = nbytes <= window_bytes(S);
+  sc.in_lds = nbytes <= window_bytes(Smax);
   sc.gw = reinterpret_cast<const uint32_t *>(dstuf + wb);
   if (sc.in_lds)
     for (int i = tid; i < (int)nbytes / 4; i += kSyncThreads) win[skew(i)] = __builtin_bswap32(sc.gw[i]);
@@ -680,7 +680,7 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
 __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
-    const int32_t *__restrict__ wg_img, int S, SubState *__restrict__ sub,
+    const int32_t *__restrict__ wg_img, int Smax, SubState *__restrict__ sub,
     const int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
   __shared__ SyncLds sh;
   __shared__ unsigned long long sh_lohi[2];
@@ -690,8 +690,9 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
   const int tid = threadIdx.x;
   SubCtx sc;
   const lds_u32 win = (lds_u32)dyn_lds;
-  const Dec dec = sub_setup(d, segs, htabs, S, dstuf, win,
-                            (lds_u16)(dyn_lds + window_lds_bytes(S) / 4), sh_lohi, sc);
+  const int S = d.sub_bits;
+  const Dec dec = sub_setup(d, segs, htabs, S, Smax, dstuf, win,
+                            (lds_u16)(dyn_lds + window_lds_bytes(Smax) / 4), sh_lohi, sc);
   int nblk;
   if (sc.in_lds) nblk = sync_lane(LdsWords{(lds_cu32)win}, sc, dec, S, sh, dbg);
   else nblk = sync_lane(GlobWords{sc.gw}, sc, dec, S, sh, dbg);
@@ -767,7 +768,7 @@ __global__ void __launch_bounds__(64) k_huff_fix(const ImgDesc *__restrict__ des
                                                  const Segment *__restrict__ segs,
                                                  const HuffTab *__restrict__ htabs,
                                                  const uint8_t *__restrict__ dstuf,
-                                                 const int32_t *__restrict__ wg_img, int S,
+                                                 const int32_t *__restrict__ wg_img, int Smax,
                                                  SubState *__restrict__ sub,
                                                  const int32_t *__restrict__ status,
                                                  int32_t *__restrict__ redo) {
@@ -787,7 +788,8 @@ __global__ void __launch_bounds__(64) k_huff_fix(const ImgDesc *__restrict__ des
   if (pv.exit_p == cand.exit_p && pv.exit_bk == cand.exit_bk) return; // helpers were right
   const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, threadIdx.x, 64);
   __syncthreads();
-  if (threadIdx.x == 0) boundary_walk(d, dec, segs, dstuf, S, sub, lt0, true, redo, redo);
+  if (threadIdx.x == 0) boundary_walk(d, dec, segs, dstuf, d.sub_bits, sub, lt0, true, redo, redo);
+  (void)Smax;
 }
 
 // Fallback when a walk did not converge inside its workgroup: one lane per
@@ -795,7 +797,7 @@ __global__ void __launch_bounds__(64) k_huff_fix(const ImgDesc *__restrict__ des
 __global__ void __launch_bounds__(64) k_huff_fix_serial(const ImgDesc *__restrict__ descs,
                                                         const Segment *__restrict__ segs,
                                                         const HuffTab *__restrict__ htabs,
-                                                        const uint8_t *__restrict__ dstuf, int S,
+                                                        const uint8_t *__restrict__ dstuf, int Smax,
                                                         SubState *__restrict__ sub,
                                                         const int32_t *__restrict__ status,
                                                         const int32_t *__restrict__ redo) {
@@ -810,7 +812,7 @@ __global__ void __launch_bounds__(64) k_huff_fix_serial(const ImgDesc *__restric
   for (int wl = 1; wl < d.wg_count; ++wl) {
     const int lt0 = wl * kSlotsPerWg;
     if (lt0 >= total) break;
-    boundary_walk(d, dec, segs, dstuf, S, sub, lt0, false, nullptr, nullptr);
+    boundary_walk(d, dec, segs, dstuf, d.sub_bits, sub, lt0, false, nullptr, nullptr);
   }
 }
 
@@ -864,7 +866,7 @@ __device__ __forceinline__ void write_lane(W src, const SubCtx &sc, const Dec &d
 __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
-    const int32_t *__restrict__ wg_img, int S, const SubState *__restrict__ sub,
+    const int32_t *__restrict__ wg_img, int Smax, const SubState *__restrict__ sub,
     const int32_t *__restrict__ pre, int16_t *__restrict__ coef,
     int16_t *__restrict__ dcv, int32_t *__restrict__ status) {
   __shared__ uint8_t s_nat[80];
@@ -876,8 +878,9 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
   if (tid < 80) s_nat[tid] = c_natural[tid];
   SubCtx sc;
   const lds_u32 win = (lds_u32)dyn_lds;
-  const Dec dec = sub_setup(d, segs, htabs, S, dstuf, win,
-                            (lds_u16)(dyn_lds + window_lds_bytes(S) / 4), sh_lohi, sc);
+  const int S = d.sub_bits;
+  const Dec dec = sub_setup(d, segs, htabs, S, Smax, dstuf, win,
+                            (lds_u16)(dyn_lds + window_lds_bytes(Smax) / 4), sh_lohi, sc);
   if (!sc.active) return;
   const Segment &sg = segs[sc.seg];
   const int64_t gt = (int64_t)blockIdx.x * kSyncThreads + tid;

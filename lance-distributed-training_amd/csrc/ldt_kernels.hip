@@ -305,7 +305,9 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
   if (subseq_bits <= 0) return;
   __syncthreads();
   // subsequence layout for the parallel Huffman decoder: segment s gets
-  // max(1, ceil(bits / S)) threads, numbered from 0 across the image.
+  // max(1, ceil(bits / S)) threads, numbered from 0 across the image, with the
+  // image's own S (the planner sizes it to fill whole workgroups).
+  const int S = d.sub_bits;
   int base = 0;
   for (int s0 = 0; s0 < d.nseg; s0 += 256) {
     const int s = s0 + tid;
@@ -313,7 +315,7 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
     if (s < d.nseg) {
       const Segment &sg = segs[d.seg_base + s];
       const int64_t bits = (sg.byte_end - sg.byte_start) * 8;
-      cnt_s = (int)((bits + subseq_bits - 1) / subseq_bits);
+      cnt_s = (int)((bits + S - 1) / S);
       if (cnt_s < 1) cnt_s = 1;
     }
     int tot;

@@ -41,7 +41,7 @@ struct ImgDesc {
   int32_t sub_cap;   // thread slots reserved (>= sum of segment sub_count)
   // destuff: this image's 4 KB chunks are [ds_first, ds_first + ds_count)
   int32_t ds_first, ds_count;
-  int32_t pad2_;
+  int32_t sub_bits;  // parallel Huffman subsequence length S of this image (bits)
 };
 
 // One entropy-coded segment (a restart interval, or the whole scan).
