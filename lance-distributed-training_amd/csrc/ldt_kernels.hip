@@ -348,7 +348,11 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
 #define FIX_3_072711026 25172
 
 // One 1-D ISLOW butterfly on in[0..7] (stride 1), producing the 8 pre-descale
-// sums in the order libjpeg stores them.
+// sums in the order libjpeg stores them. Every multiply is var x FIX_* with
+// |var| < 2^23 (pass 1: dequantised 11-bit coefficients x 8-bit quant, sums
+// of <= 4; pass 2: int16 workspace values, see k_idct), so the products are
+// exact 24-bit multiplies (v_mul_i32_i24, full rate; a plain int multiply
+// becomes the quarter-rate v_mul_lo_u32).
 struct Islow8 {
   int32_t o[8];
 };
@@ -356,9 +360,9 @@ __device__ __forceinline__ Islow8 islow_1d(const int32_t *x, int pass1) {
   int32_t tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13, z1, z2, z3, z4, z5;
   z2 = x[2];
   z3 = x[6];
-  z1 = (z2 + z3) * FIX_0_541196100;
-  tmp2 = z1 + z3 * (-FIX_1_847759065);
-  tmp3 = z1 + z2 * FIX_0_765366865;
+  z1 = __mul24(z2 + z3, FIX_0_541196100);
+  tmp2 = z1 + __mul24(z3, -FIX_1_847759065);
+  tmp3 = z1 + __mul24(z2, FIX_0_765366865);
   tmp0 = (x[0] + x[4]) * (1 << 13);
   tmp1 = (x[0] - x[4]) * (1 << 13);
   tmp10 = tmp0 + tmp3;
@@ -373,15 +377,15 @@ __device__ __forceinline__ Islow8 islow_1d(const int32_t *x, int pass1) {
   z2 = tmp1 + tmp2;
   z3 = tmp0 + tmp2;
   z4 = tmp1 + tmp3;
-  z5 = (z3 + z4) * FIX_1_175875602;
-  tmp0 = tmp0 * FIX_0_298631336;
-  tmp1 = tmp1 * FIX_2_053119869;
-  tmp2 = tmp2 * FIX_3_072711026;
-  tmp3 = tmp3 * FIX_1_501321110;
-  z1 = z1 * (-FIX_0_899976223);
-  z2 = z2 * (-FIX_2_562915447);
-  z3 = z3 * (-FIX_1_961570560);
-  z4 = z4 * (-FIX_0_390180644);
+  z5 = __mul24(z3 + z4, FIX_1_175875602);
+  tmp0 = __mul24(tmp0, FIX_0_298631336);
+  tmp1 = __mul24(tmp1, FIX_2_053119869);
+  tmp2 = __mul24(tmp2, FIX_3_072711026);
+  tmp3 = __mul24(tmp3, FIX_1_501321110);
+  z1 = __mul24(z1, -FIX_0_899976223);
+  z2 = __mul24(z2, -FIX_2_562915447);
+  z3 = __mul24(z3, -FIX_1_961570560);
+  z4 = __mul24(z4, -FIX_0_390180644);
   z3 += z5;
   z4 += z5;
   tmp0 += z1 + z3;
@@ -400,6 +404,11 @@ __device__ __forceinline__ Islow8 islow_1d(const int32_t *x, int pass1) {
   (void)pass1;
   return r;
 }
+
+// The pass-1 workspace is 16-bit in libjpeg-turbo's SIMD ISLOW (the path
+// Pillow runs on x86-64: packssdw after pass 1); for valid data the values fit
+// and this is the identity, and it bounds the pass-2 multiplies to 24 bits.
+__device__ __forceinline__ int32_t sat16(int32_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
 
 // jdmaster.c prepare_range_limit_table, post-IDCT part, indexed by x & 1023:
 // [0,128) -> x + 128, [128,512) -> 255, [512,896) -> 0, [896,1024) -> x - 896,
@@ -491,9 +500,9 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
       for (int j = 0; j < 8; ++j) x[j] = ws[8 * j + c];
       const Islow8 t = islow_1d(x, 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ws[8 * j + c] = (t.o[j] + (1 << 10)) >> 11; // DESCALE(, 13-2)
+      for (int j = 0; j < 8; ++j) ws[8 * j + c] = sat16((t.o[j] + (1 << 10)) >> 11); // DESCALE(, 13-2)
     } else {
-      const int32_t dc4 = ws[c] * 4;
+      const int32_t dc4 = sat16(ws[c] * 4);
 #pragma unroll
       for (int j = 0; j < 8; ++j) ws[8 * j + c] = dc4;
     }

@@ -140,9 +140,9 @@ __device__ __forceinline__ void stage8_jpeg(const ImgDesc &d, const uint8_t *__r
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int xcr = Cr[j] - 128, xcb = Cb[j] - 128;
-        const int R = clampi(Y[j] + ((91881 * xcr + 32768) >> 16), 0, 255);
-        const int G = clampi(Y[j] + ((-22554 * xcb + 32768 + (-46802) * xcr) >> 16), 0, 255);
-        const int B = clampi(Y[j] + ((116130 * xcb + 32768) >> 16), 0, 255);
+        const int R = clampi(Y[j] + ((__mul24(91881, xcr) + 32768) >> 16), 0, 255);
+        const int G = clampi(Y[j] + ((__mul24(-22554, xcb) + 32768 + __mul24(-46802, xcr)) >> 16), 0, 255);
+        const int B = clampi(Y[j] + ((__mul24(116130, xcb) + 32768) >> 16), 0, 255);
         px[j] = rgbx(R, G, B);
       }
     }
@@ -320,10 +320,10 @@ __global__ void __launch_bounds__(256) k_resize3(const ImgDesc *__restrict__ des
 #pragma unroll
           for (int t = 0; t < KS; ++t) {
             const uint32_t v = src[t];
-            const int32_t kw = wgt[q][t];
-            a0 += (int32_t)(v & 255) * kw;
-            a1 += (int32_t)((v >> 8) & 255) * kw;
-            a2 += (int32_t)((v >> 16) & 255) * kw;
+            const uint32_t kw = (uint32_t)wgt[q][t]; // Pillow weights: 0 <= kw <= 2^22
+            a0 += (int32_t)__umul24(v & 255, kw);
+            a1 += (int32_t)__umul24((v >> 8) & 255, kw);
+            a2 += (int32_t)__umul24((v >> 16) & 255, kw);
           }
           s_tmp[(0 * ring + slot) * kOut + ox] = (uint8_t)clip8(a0);
           s_tmp[(1 * ring + slot) * kOut + ox] = (uint8_t)clip8(a1);
@@ -343,11 +343,11 @@ __global__ void __launch_bounds__(256) k_resize3(const ImgDesc *__restrict__ des
         for (int t = 0; t < cnt; ++t) {
           const int slot = (ymin + t) & (ring - 1);
           const uint32_t v = *reinterpret_cast<const uint32_t *>(s_tmp + (vc * ring + slot) * kOut + vox4);
-          const int32_t kw = kv[t];
-          a0 += (int32_t)(v & 255) * kw;
-          a1 += (int32_t)((v >> 8) & 255) * kw;
-          a2 += (int32_t)((v >> 16) & 255) * kw;
-          a3 += (int32_t)(v >> 24) * kw;
+          const uint32_t kw = (uint32_t)kv[t];
+          a0 += (int32_t)__umul24(v & 255, kw);
+          a1 += (int32_t)__umul24((v >> 8) & 255, kw);
+          a2 += (int32_t)__umul24((v >> 16) & 255, kw);
+          a3 += (int32_t)__umul24(v >> 24, kw);
         }
         const float *lc = s_lut + vc * 256;
         float4 f;

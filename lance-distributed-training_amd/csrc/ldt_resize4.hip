@@ -46,11 +46,13 @@ __device__ __forceinline__ uint32_t rgbx(int r, int g, int b) {
 }
 
 // jdcolor.c ycc_rgb_convert (16-bit fixed point, ONE_HALF in the Cb->G term).
+// Every factor fits 24 bits, so the products are v_mul_i32_i24 (full rate)
+// rather than the quarter-rate v_mul_lo_u32 the compiler would pick.
 __device__ __forceinline__ uint32_t ycc_px(int y, int cb, int cr) {
   const int xcr = cr - 128, xcb = cb - 128;
-  const int r = y + ((91881 * xcr + 32768) >> 16);
-  const int g = y + ((-22554 * xcb + 32768 + (-46802) * xcr) >> 16);
-  const int b = y + ((116130 * xcb + 32768) >> 16);
+  const int r = y + ((__mul24(91881, xcr) + 32768) >> 16);
+  const int g = y + ((__mul24(-22554, xcb) + 32768 + __mul24(-46802, xcr)) >> 16);
+  const int b = y + ((__mul24(116130, xcb) + 32768) >> 16);
   return rgbx(clampi(r, 0, 255), clampi(g, 0, 255), clampi(b, 0, 255));
 }
 
@@ -376,11 +378,13 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
       int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
+        // Pillow weights are >= 0 and <= 2^22: 24-bit products (v_mul_u32_u24
+        // with SDWA byte selects), exact in 32 bits
         const uint32_t v = src[t];
-        const int32_t kw = wgt[q][t];
-        a0 += (int32_t)(v & 255) * kw;
-        a1 += (int32_t)((v >> 8) & 255) * kw;
-        a2 += (int32_t)((v >> 16) & 255) * kw;
+        const uint32_t kw = (uint32_t)wgt[q][t];
+        a0 += (int32_t)__umul24(v & 255, kw);
+        a1 += (int32_t)__umul24((v >> 8) & 255, kw);
+        a2 += (int32_t)__umul24((v >> 16) & 255, kw);
       }
       const int sl = r ? slot1 : slot;
       uint8_t *rw = ring + sl * kOut + ox;
@@ -416,15 +420,15 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[i][e] = 1 << (kPrecisionBits - 1);
       for (int t = 0; t < cnt; ++t) {
-        const int32_t kw = __builtin_amdgcn_readfirstlane(kv[jr * ks_v + t]);
+        const uint32_t kw = (uint32_t)__builtin_amdgcn_readfirstlane(kv[jr * ks_v + t]);
         const int sl = s0 + t < RING ? s0 + t : s0 + t - RING;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           const uint32_t v = *reinterpret_cast<const uint32_t *>(ring + (vc[i] * RING + sl) * kOut + vo[i]);
-          acc[i][0] += (int32_t)(v & 255) * kw;
-          acc[i][1] += (int32_t)((v >> 8) & 255) * kw;
-          acc[i][2] += (int32_t)((v >> 16) & 255) * kw;
-          acc[i][3] += (int32_t)(v >> 24) * kw;
+          acc[i][0] += (int32_t)__umul24(v & 255, kw);
+          acc[i][1] += (int32_t)__umul24((v >> 8) & 255, kw);
+          acc[i][2] += (int32_t)__umul24((v >> 16) & 255, kw);
+          acc[i][3] += (int32_t)__umul24(v >> 24, kw);
         }
       }
 #pragma unroll
