@@ -64,6 +64,9 @@ extern "C" {
                                  caller's stream (read with ldt_stage_times)    */
 #define LDT_OPT_RESIZE_IMPL 5 /* 0 auto (default): one wave per band; 2: the
                                  banded workgroup kernel (cross-check)          */
+#define LDT_OPT_SUBSEQ_FIT 6  /* 1 (default): per image, shrink the subsequence
+                                 length so its slots fill whole workgroups;
+                                 0: every image uses LDT_OPT_SUBSEQ_BITS        */
 
 /* ---- stages reported by ldt_stage_times ---- */
 #define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */

@@ -271,6 +271,7 @@ struct ldt_ctx {
   bool sync_status = true;
   int huff_mode = 0;
   int resize_impl = 0;
+  bool subseq_fit = true;
   int subseq_bits = 1024;
   DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_sub, d_pre, d_dscnt;
   bool coef_dirty = false; // a batch wrote coefficients but k_idct did not run
@@ -643,7 +644,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       // S <= the context's S that still fills its last workgroup (fewer,
       // fuller workgroups; S stays within the LDS window sized for SB)
       int64_t sbits = SB;
-      if (d.nseg == 1 && SB >= 256) {
+      if (c->subseq_fit && d.nseg == 1 && SB >= 256) {
         const int64_t bits = d.src_len * 8;
         const int64_t k = std::max<int64_t>(1, (bits + (int64_t)SB * (kSlotsPerWg - 1) - 1) /
                                                    ((int64_t)SB * (kSlotsPerWg - 1)));
@@ -909,6 +910,9 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     return LDT_OK;
   case LDT_OPT_PROFILE:
     c->profile = value != 0;
+    return LDT_OK;
+  case LDT_OPT_SUBSEQ_FIT:
+    c->subseq_fit = value != 0;
     return LDT_OK;
   case LDT_OPT_RESIZE_IMPL:
     if (value != 0 && value != 2) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);

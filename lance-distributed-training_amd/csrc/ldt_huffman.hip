@@ -236,33 +236,79 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
   advance(st, dec, (int)(e >> 9));
 }
 
+// Coefficients of a block are stored in zigzag (decode) order, int16 slots
+// 1..63 (DC lives in dcv); k_idct de-zigzags while dequantising. Slots are
+// combined 8 at a time (16 bytes) in registers and written with one store per
+// touched group instead of one 2-byte scatter per coefficient: a block's
+// coefficient indices only grow, so a group is complete once the index leaves
+// it or the block ends. Groups a neighbouring range may also write (a block
+// straddling the range boundary) are written slot by slot.
+__device__ __forceinline__ void store_group(int16_t *__restrict__ p, uint64_t lo, uint64_t hi) {
+#ifdef LDT_EXP_NOSTORE // experiment build: time the decode without coefficient stores
+  if (lo == 0x0123456789abcdefull) *reinterpret_cast<uint4 *>(p) = make_uint4(0, 0, 0, 0);
+  return;
+#endif
+  *reinterpret_cast<uint4 *>(p) =
+      make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
 // Coefficient-writing decode of one range: from the reader's position until
 // it reaches `stop` or the segment's `total` blocks are complete. cursor is
 // the current block (segment-relative, -1 before the first DC). DC symbols
 // store their difference in dcv_seg[cursor] (k_dc_scan adds the predictors);
 // nonzero AC coefficients go to coef_seg, which is all zero beforehand
-// (k_idct clears every block it reads).
-template <class W, class NAT>
+// (k_idct clears every block it reads). The loop body is straight-line: every
+// store is predicated, so a wave branches only around stores no lane makes.
+template <class W>
 __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
-                                          int64_t &cursor, int64_t total,
-                                          int16_t *__restrict__ coef_seg,
-                                          int16_t *__restrict__ dcv_seg, NAT nat) {
-  while (R.p < stop) {
-    if (st.k == 0) {
-      if (cursor + 1 >= total) break;
-      ++cursor;
-    }
+                                          int &cursor, int total, int16_t *__restrict__ coef_seg,
+                                          int16_t *__restrict__ dcv_seg) {
+  uint64_t lo = 0, hi = 0; // buffered group: slots 0-3, 4-7
+  int grp = -1;            // its index (slot >> 3), -1 = empty
+  // entered mid-block: the previous range may have written this group of it
+  const int shared_g = st.k != 0 ? (st.k >> 3) : -1;
+  bool first = true;       // still in the block the range entered
+  bool go = R.p < stop && !(st.k == 0 && cursor + 1 >= total);
+  while (go) {
+    const bool dc = st.k == 0;
+    cursor += dc ? 1 : 0;
     const uint32_t pk = R.peek();
     const uint32_t e = lookup(dec, st, pk);
     const int v = ext_value(pk, e);
     const int adv = (int)(e >> 9);
-    if (st.k == 0) {
-      dcv_seg[cursor] = (int16_t)v;
-    } else if ((e >> 5) & 15) {
-      if (cursor >= 0) coef_seg[cursor * 64 + nat[st.k + adv - 1]] = (int16_t)v;
-    }
+    const bool nz = !dc && ((e >> 5) & 15) != 0;
+    const int slot = st.k + adv - 1;
+    const int g = slot >> 3;
+    int16_t *__restrict__ blk = coef_seg + (int64_t)cursor * 64;
+    if (dc) dcv_seg[cursor] = (int16_t)v;
+    const bool direct = nz && first && g == shared_g;
+#ifndef LDT_EXP_NOSTORE
+    if (direct) blk[slot] = (int16_t)v;
+#endif
+    const bool buf = nz && !direct;
+    const bool newg = buf && g != grp;
+    if (newg && grp >= 0) store_group(blk + 8 * grp, lo, hi);
+    lo = newg ? 0ull : lo;
+    hi = newg ? 0ull : hi;
+    grp = newg ? g : grp;
+    const uint64_t x = buf ? (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3)) : 0ull;
+    lo |= (slot & 4) ? 0ull : x;
+    hi |= (slot & 4) ? x : 0ull;
     R.consume((int)(e & 31));
+    const bool end = st.k + adv >= 64;
+    if (end && grp >= 0) store_group(blk + 8 * grp, lo, hi);
+    grp = end ? -1 : grp;
+    first = first && !end;
     advance(st, dec, adv);
+    go = R.p < stop && !(st.k == 0 && cursor + 1 >= total);
+  }
+  if (grp >= 0) { // the open block continues in the next range
+    int16_t *p = coef_seg + (int64_t)cursor * 64 + 8 * grp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint16_t x = (uint16_t)(((j & 4) ? hi : lo) >> (16 * (j & 3)));
+      if (x) p[j] = (int16_t)x;
+    }
   }
 }
 
@@ -276,12 +322,10 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
                                                     int16_t *__restrict__ coef,
                                                     int16_t *__restrict__ dcv,
                                                     int32_t *__restrict__ status) {
-  __shared__ uint8_t s_nat[80];
   const int img = blockIdx.x;
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
-  for (int i = tid; i < 80; i += 64) s_nat[i] = c_natural[i];
   const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, tid, 64);
   __syncthreads();
   for (int si = d.seg_base + tid; si < d.seg_base + d.nseg; si += 64) {
@@ -292,12 +336,11 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
     const int32_t pbias = (int32_t)(sg.byte_start & 3) * 8;
     R.seek(pbias);
     St st = make_state(0);
-    const int64_t total = (int64_t)sg.mcu_count * d.bpm;
-    int64_t cursor = -1;
+    const int total = sg.mcu_count * d.bpm;
+    int cursor = -1;
     const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
     // a valid segment ends inside its bits; 64 bits of slack bound a corrupt one
-    write_run(R, st, dec, pbias + seg_bits + 64, cursor, total, coef + blk0 * 64, dcv + blk0,
-              (lds_cu8)s_nat);
+    write_run(R, st, dec, pbias + seg_bits + 64, cursor, total, coef + blk0 * 64, dcv + blk0);
     if (R.p - pbias > seg_bits || cursor + 1 < total || st.k != 0) status[img] = 3; // truncated
   }
 }
@@ -847,17 +890,17 @@ __global__ void __launch_bounds__(256) k_huff_scan(const ImgDesc *__restrict__ d
 template <class W>
 __device__ __forceinline__ void write_lane(W src, const SubCtx &sc, const Dec &dec, int S,
                                            const ImgDesc &d, const Segment &sg, int entry, int bk,
-                                           int64_t cursor, int16_t *__restrict__ coef,
-                                           int16_t *__restrict__ dcv, lds_cu8 nat,
+                                           int cursor, int16_t *__restrict__ coef,
+                                           int16_t *__restrict__ dcv,
                                            int32_t *__restrict__ status, int img) {
   St st = make_state(bk);
-  const int64_t total = (int64_t)sg.mcu_count * d.bpm;
+  const int total = sg.mcu_count * d.bpm;
   const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
   Rd<W> R;
   R.src = src;
   R.seek(sc.pbias + entry);
   write_run(R, st, dec, sc.pbias + min((sc.j + 1) * S, sc.seg_bits), cursor, total,
-            coef + blk0 * 64, dcv + blk0, nat);
+            coef + blk0 * 64, dcv + blk0);
   if (sc.j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
 }
 
@@ -869,13 +912,11 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
     const int32_t *__restrict__ wg_img, int Smax, const SubState *__restrict__ sub,
     const int32_t *__restrict__ pre, int16_t *__restrict__ coef,
     int16_t *__restrict__ dcv, int32_t *__restrict__ status) {
-  __shared__ uint8_t s_nat[80];
   __shared__ unsigned long long sh_lohi[2];
   const int img = wg_img[blockIdx.x];
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
-  if (tid < 80) s_nat[tid] = c_natural[tid];
   SubCtx sc;
   const lds_u32 win = (lds_u32)dyn_lds;
   const int S = d.sub_bits;
@@ -891,13 +932,13 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_write(
     entry = ps.exit_p;
     bk = ps.exit_bk;
   }
-  const int64_t cursor = (int64_t)(pre[gt] - pre[slot_gt(d, sg.sub_first)]) - 1;
+  const int cursor = pre[gt] - pre[slot_gt(d, sg.sub_first)] - 1;
   if (sc.in_lds)
     write_lane(LdsWords{(lds_cu32)win}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv,
-               (lds_cu8)s_nat, status, img);
+               status, img);
   else
     write_lane(GlobWords{sc.gw}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv,
-               (lds_cu8)s_nat, status, img);
+               status, img);
 }
 
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {

@@ -430,6 +430,11 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
 // every block it reads (also for images whose decode failed), so the buffer
 // needs no memset per batch (it is cleared once when allocated).
 constexpr int kIdctBlocksPerWg = 256;
+// jpeg_natural_order: zigzag position -> natural (row-major) index
+constexpr int kZigzagNat[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 constexpr int kIdctTileStride = 36; // dwords per block in the LDS tile
 
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
@@ -462,7 +467,8 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
     }
   }
   if (!ok) return; // failed image: only restore the all-zero invariant
-  if (tid < 64 * d.ncomp) s_q[tid >> 6][tid & 63] = qtabs[d.qt[tid >> 6] * 64 + (tid & 63)];
+  // quant tables in zigzag order, like the coefficients
+  if (tid < 64 * d.ncomp) s_q[tid >> 6][tid & 63] = qtabs[d.qt[tid >> 6] * 64 + kZigzagNat[tid & 63]];
   __syncthreads();
   if (tid >= nb) return;
   const int64_t blk = b0 + tid;
@@ -470,7 +476,8 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
   const int b = (int)(blk - m * d.bpm);
   const int comp = d.bcomp[b];
   const uint16_t *q = s_q[comp];
-  // dequantised block, row-major (jidctint.c DEQUANTIZE)
+  // dequantised block, row-major (jidctint.c DEQUANTIZE); the stored slots
+  // are in zigzag order (k_huff_write), placed at their natural index here
   int32_t ws[64];
   const uint32_t *tl = &s_tile[tid * kIdctTileStride];
 #pragma unroll
@@ -482,8 +489,8 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int32_t lo = (int32_t)(int16_t)(rw[j] & 0xFFFF), hi = (int32_t)(int16_t)(rw[j] >> 16);
-      ws[8 * r + 2 * j] = lo * (int32_t)(qw[j] & 0xFFFF);
-      ws[8 * r + 2 * j + 1] = hi * (int32_t)(qw[j] >> 16);
+      ws[kZigzagNat[8 * r + 2 * j]] = __mul24(lo, (int32_t)(qw[j] & 0xFFFF));
+      ws[kZigzagNat[8 * r + 2 * j + 1]] = __mul24(hi, (int32_t)(qw[j] >> 16));
     }
   }
   ws[0] = (int32_t)dcv[d.coef_off + blk] * (int32_t)q[0]; // DC: absolute value from k_dc_scan

@@ -42,6 +42,7 @@ OPT_HUFF_MODE = 2
 OPT_SUBSEQ_BITS = 3
 OPT_PROFILE = 4
 OPT_RESIZE_IMPL = 5
+OPT_SUBSEQ_FIT = 6
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
 
@@ -88,7 +89,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
     with _lib_lock:
         if _lib is not None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("LDT_LIBRARY") or LIB_PATH  # override: experiment builds
         if not os.path.exists(p):
             raise ImportError(
                 f"libldt.so not found at {p}: build it with `make -C lance-distributed-training_amd` "
