@@ -157,6 +157,8 @@ def main():
         for c in pipe.ctxs:  # tuning knobs (defaults: S = 1024 bits, fitted per image)
             if os.environ.get("LDT_SUBSEQ_BITS"):
                 c.set_option(_lib.OPT_SUBSEQ_BITS, int(os.environ["LDT_SUBSEQ_BITS"]))
+            if os.environ.get("LDT_SYNC_WARM"):
+                c.set_option(_lib.OPT_SYNC_WARM, int(os.environ["LDT_SYNC_WARM"]))
             if os.environ.get("LDT_SUBSEQ_FIT"):
                 c.set_option(_lib.OPT_SUBSEQ_FIT, int(os.environ["LDT_SUBSEQ_FIT"]))
 

@@ -67,6 +67,8 @@ extern "C" {
 #define LDT_OPT_SUBSEQ_FIT 6  /* 1 (default): per image, shrink the subsequence
                                  length so its slots fill whole workgroups;
                                  0: every image uses LDT_OPT_SUBSEQ_BITS        */
+#define LDT_OPT_SYNC_WARM 7   /* parallel decoder phase 1 starts this % of S
+                                 before each range (0..200, default 0)         */
 
 /* ---- stages reported by ldt_stage_times ---- */
 #define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */

@@ -272,6 +272,7 @@ struct ldt_ctx {
   int huff_mode = 0;
   int resize_impl = 0;
   bool subseq_fit = true;
+  int warm_pct = 0;
   int subseq_bits = 1024;
   DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_sub, d_pre, d_dscnt;
   bool coef_dirty = false; // a batch wrote coefficients but k_idct did not run
@@ -780,6 +781,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.max_h = max_h;
   p.max_blocks = max_blocks;
   p.subseq_bits = parallel ? SB : 0;
+  p.warm_pct = c->warm_pct;
   p.n_wg = parallel ? n_wg : 0;
   p.wg_img = reinterpret_cast<const int32_t *>(dp + off_wg);
   p.n_chunks = n_chunks;
@@ -910,6 +912,10 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     return LDT_OK;
   case LDT_OPT_PROFILE:
     c->profile = value != 0;
+    return LDT_OK;
+  case LDT_OPT_SYNC_WARM:
+    if (value < 0 || value > 200) return set_err(c, LDT_ERR_ARG, "sync warm-up %lld", (long long)value);
+    c->warm_pct = (int)value;
     return LDT_OK;
   case LDT_OPT_SUBSEQ_FIT:
     c->subseq_fit = value != 0;

@@ -647,13 +647,23 @@ __device__ __forceinline__ bool count_run(Rd<W> &R, int32_t range_start, int32_t
 struct SyncLds {
   int32_t ex_p[kSyncThreads];
   uint16_t ex_bk[kSyncThreads]; // (3b << 8) | k <= 27 * 256 + 63
-  uint8_t chg[kSyncThreads];
   int any_changed;
 };
 
 // Phase 1 + intra-workgroup convergence for one lane; returns its block count.
+//
+// Phase 1 starts `warm` bits before the lane's range (never before its segment
+// or the window) from a guessed state (b = 0, k = 0), so the trajectory has
+// usually resynchronised by the range start; the lane records its entry state
+// (first symbol boundary at/after the range start) and its exit. A lane then
+// re-decodes only while its entry differs from its predecessor's exit, and a
+// re-decode stops at the first checkpoint where it merges with the lane's own
+// previous trajectory. The warm-up trades one extra range of decoding in phase
+// 1 for chains of wrong exits that are much rarer (they need a resync distance
+// above warm + S instead of S), which cuts the rounds of the slowest
+// workgroup, and with them the kernel's latency.
 template <class W>
-__device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec, int S,
+__device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec, int S, int warm,
                                          SyncLds &sh, int32_t *__restrict__ dbg) {
   const int tid = threadIdx.x;
   int nblk = 0;
@@ -665,10 +675,17 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
   R.src = src;
   const int32_t rstart = sc.pbias + sc.j * S;
   const int32_t stop = sc.pbias + min((sc.j + 1) * S, sc.seg_bits);
-  // phase 1: every slot and helper decodes its range from a guessed state
-  // (b = 0, k = 0 at the range start); j == 0 starts exactly.
-  if (sc.active || sc.helper) {
-    R.seek(rstart);
+  const bool live = sc.active || sc.helper;
+  int en_p = 0, en_bk = 0; // state at the range start (segment-relative position)
+  if (live) {
+    const int32_t w0 = max(rstart - warm, max(sc.pbias, 0));
+    R.seek(w0);
+    if (w0 < rstart) {
+      int skipped = 0;
+      count_until(R, rstart, st, dec, skipped);
+    }
+    en_p = R.p - sc.pbias;
+    en_bk = st.bk();
     count_run<false>(R, rstart, stop, S, st, dec, nblk, cp, none, 0);
     sh.ex_p[tid] = R.p - sc.pbias;
     sh.ex_bk[tid] = (uint16_t)st.bk();
@@ -676,8 +693,6 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
     sh.ex_p[tid] = 0;
     sh.ex_bk[tid] = 0;
   }
-  // every lane with an in-workgroup predecessor in its segment re-decodes
-  bool need = (sc.active || sc.helper) && sc.j > 0 && tid > 0;
   int rounds = 0;
   for (int round = 0; round < kSyncThreads + 1; ++round) {
     ++rounds;
@@ -685,13 +700,16 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
     if (tid == 0) sh.any_changed = 0;
     bool changed = false;
     int np = 0, nbk = 0;
+    const bool need = live && sc.j > 0 && tid > 0 &&
+                      (sh.ex_p[tid - 1] != en_p || sh.ex_bk[tid - 1] != en_bk);
     if (need) {
-      const int ep = sh.ex_p[tid - 1], ebk = sh.ex_bk[tid - 1];
-      st = make_state(ebk);
+      en_p = sh.ex_p[tid - 1];
+      en_bk = sh.ex_bk[tid - 1];
+      st = make_state(en_bk);
       const int prev_total = nblk;
       const Cp prev = cp;
       nblk = 0;
-      R.seek(sc.pbias + ep);
+      R.seek(sc.pbias + en_p);
       if (count_run<true>(R, rstart, stop, S, st, dec, nblk, cp, prev, prev_total)) {
         np = sh.ex_p[tid];
         nbk = sh.ex_bk[tid];
@@ -702,7 +720,6 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
       changed = (np != sh.ex_p[tid]) || (nbk != sh.ex_bk[tid]);
     }
     __syncthreads();
-    sh.chg[tid] = changed ? 1 : 0;
     if (changed) {
       sh.ex_p[tid] = np;
       sh.ex_bk[tid] = (uint16_t)nbk;
@@ -710,7 +727,6 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
     }
     __syncthreads();
     if (!sh.any_changed) break;
-    need = (sc.active || sc.helper) && sc.j > 0 && tid > 0 && sh.chg[tid > 0 ? tid - 1 : 0];
   }
   if (dbg && tid == 0) {
     atomicAdd(dbg + 1, 1);
@@ -723,7 +739,7 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
 __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
-    const int32_t *__restrict__ wg_img, int Smax, SubState *__restrict__ sub,
+    const int32_t *__restrict__ wg_img, int Smax, int warm_pct, SubState *__restrict__ sub,
     const int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
   __shared__ SyncLds sh;
   __shared__ unsigned long long sh_lohi[2];
@@ -737,8 +753,9 @@ __global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
   const Dec dec = sub_setup(d, segs, htabs, S, Smax, dstuf, win,
                             (lds_u16)(dyn_lds + window_lds_bytes(Smax) / 4), sh_lohi, sc);
   int nblk;
-  if (sc.in_lds) nblk = sync_lane(LdsWords{(lds_cu32)win}, sc, dec, S, sh, dbg);
-  else nblk = sync_lane(GlobWords{sc.gw}, sc, dec, S, sh, dbg);
+  const int warm = (S * warm_pct) / 100;
+  if (sc.in_lds) nblk = sync_lane(LdsWords{(lds_cu32)win}, sc, dec, S, warm, sh, dbg);
+  else nblk = sync_lane(GlobWords{sc.gw}, sc, dec, S, warm, sh, dbg);
   if (sc.active || tid == kHelpers - 1) {
     SubState s;
     s.exit_p = sh.ex_p[tid];
@@ -946,7 +963,7 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
   const size_t tab_lds = (size_t)(p.max_tabs < 1 ? 1 : p.max_tabs) * kTabU16 * 2;
   const size_t dec_lds = (size_t)window_lds_bytes(p.subseq_bits) + tab_lds;
   hipLaunchKernelGGL(k_huff_sync, dim3(p.n_wg), dim3(kSyncThreads), dec_lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.status, p.redo);
+                     p.htabs, w.dstuf, p.wg_img, p.subseq_bits, p.warm_pct, w.sub, w.status, p.redo);
   hipLaunchKernelGGL(k_huff_fix, dim3(p.n_wg), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,
                      w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.status, p.redo);
   hipLaunchKernelGGL(k_huff_fix_serial, dim3(p.n), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,

@@ -31,6 +31,7 @@ struct DevPlan {
   int64_t max_blocks;
   // parallel Huffman decode
   int subseq_bits;
+  int warm_pct;          // sync phase-1 warm-up before each range, % of S
   int n_wg;              // total subsequence workgroups
   const int32_t *wg_img; // workgroup -> image
   int32_t *redo;         // set when a workgroup-boundary walk did not converge
