@@ -89,8 +89,18 @@ __device__ __forceinline__ Raw16 load16_any(const uint8_t *row, int W, int x0) {
   return r;
 }
 
-// 16 packed RGB pixels -> 16 RGBx dwords at row[x0..x0+16). The byte above B
-// is left as whatever follows (the taps read bytes 0..2 only).
+// Staging rows are skewed by 4 dwords per 32 pixels: the horizontal taps of
+// neighbouring output columns start ~scale pixels apart, and for 224-wide
+// outputs of 512 / 1024 (scale 16/7, 32/7) every 7th lane would otherwise hit
+// the same LDS bank (4-5-way conflicts on every tap). Blocks of 8 or 16
+// pixels starting at a multiple of 8 stay contiguous and 16-byte aligned.
+template <bool SKEW = true> __device__ __forceinline__ int skw(int x) {
+  return SKEW ? x + ((x >> 5) << 2) : x;
+}
+
+// 16 packed RGB pixels -> 16 RGBx dwords at pixels [x0, x0+16) of a staging
+// row. The byte above B is left as whatever follows (the taps read bytes 0..2).
+template <bool SKEW>
 __device__ __forceinline__ void stage16_raw(const Raw16 &r, uint32_t *row, int x0) {
   const uint32_t w[13] = {r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w,
                           r.c.x, r.c.y, r.c.z, r.c.w, 0u};
@@ -100,7 +110,7 @@ __device__ __forceinline__ void stage16_raw(const Raw16 &r, uint32_t *row, int x
     const int o = 3 * j;
     px[j] = __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], (uint32_t)(o & 3));
   }
-  uint4 *d = reinterpret_cast<uint4 *>(row + x0);
+  uint4 *d = reinterpret_cast<uint4 *>(row + skw<SKEW>(x0));
 #pragma unroll
   for (int q = 0; q < 4; ++q) d[q] = make_uint4(px[4 * q], px[4 * q + 1], px[4 * q + 2], px[4 * q + 3]);
 }
@@ -133,7 +143,7 @@ __device__ __forceinline__ void bytes6(uint32_t w, int lane, int rc, int s[6]) {
 
 struct Geom4 {
   int nbands, bh;  // bands per image, output rows per band
-  int ring;        // intermediate ring rows (>= ks_v + 3)
+  int ring;        // intermediate ring rows (>= ks_v + 1)
   int ks_v;        // vertical taps (max over the batch)
   int spad;        // staging row stride in dwords (multiple of 4)
   int ntask;       // n * nbands
@@ -151,6 +161,10 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
                                                  int64_t *__restrict__ out_labels,
                                                  const int32_t *__restrict__ status, Geom4 g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // Skewed staging for raw rows (c5: 4-5-way tap conflicts otherwise, and the
+  // kernel is LDS-bound). JPEG rows stay plain: the skew's extra registers
+  // cost a wave per SIMD there, which is worth more than its 2-way conflicts.
+  constexpr bool kSkew = SRC == 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
   for (int i = tid; i < 768; i += 256) s_lut[i] = lut[i];
@@ -191,6 +205,13 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
     resample_coeffs_one(W, kOut, ox, KS, k, &xm[q]);
 #pragma unroll
     for (int t = 0; t < KS; ++t) wgt[q][t] = k[t];
+  }
+  // skewed staging address of each window start, and the first tap past a skew step
+  int xsk[4], xcr[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    xsk[q] = skw<kSkew>(xm[q]);
+    xcr[q] = 32 - (xm[q] & 31);
   }
   // band source rows
   int ya, yb;
@@ -234,9 +255,12 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   }
 
   // ---- prefetch helpers ----
-  Jpair jp;
-  Raw16 rp0, rp1;
-  auto fetch = [&](int y) {
+  struct Pre {
+    Jpair jp;
+    Raw16 r0, r1;
+  } pa;
+  auto fetch = [&](Pre &pf, int y) {
+    Jpair &jp = pf.jp;
     if constexpr (SRC == 0) {
       if (fast420) {
         const ImgDesc &d = *dp;
@@ -261,15 +285,16 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
       if (raw_al16) {
         const int x0 = lane * 16;
         if (x0 < W) {
-          rp0 = load16_aligned(raw_cell + (int64_t)y * W * 3 + 3 * x0);
-          if (y + 1 < H) rp1 = load16_aligned(raw_cell + (int64_t)(y + 1) * W * 3 + 3 * x0);
+          pf.r0 = load16_aligned(raw_cell + (int64_t)y * W * 3 + 3 * x0);
+          if (y + 1 < H) pf.r1 = load16_aligned(raw_cell + (int64_t)(y + 1) * W * 3 + 3 * x0);
         }
       }
     }
   };
 
   // ---- staging of one row pair into stg[0..spad) / stg[spad..2 spad) ----
-  auto stage = [&](int y) {
+  auto stage = [&](const Pre &pf, int y) {
+    const Jpair &jp = pf.jp;
     uint32_t *s0 = stg, *s1 = stg + g.spad;
     if constexpr (SRC == 0) {
       const ImgDesc &d = *dp;
@@ -308,8 +333,8 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
           p1[j] = ycc_px((int)((yb_ >> sh) & 255), cb[1][j], crr[1][j]);
         }
         if (x0 < W) {
-          uint4 *d0 = reinterpret_cast<uint4 *>(s0 + x0);
-          uint4 *d1 = reinterpret_cast<uint4 *>(s1 + x0);
+          uint4 *d0 = reinterpret_cast<uint4 *>(s0 + skw<kSkew>(x0));
+          uint4 *d1 = reinterpret_cast<uint4 *>(s1 + skw<kSkew>(x0));
           d0[0] = make_uint4(p0[0], p0[1], p0[2], p0[3]);
           d0[1] = make_uint4(p0[4], p0[5], p0[6], p0[7]);
           d1[0] = make_uint4(p1[0], p1[1], p1[2], p1[3]);
@@ -336,7 +361,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
                 px[j] = d.color == 1 ? rgbx(Y, cb, cr) : ycc_px(Y, cb, cr);
               }
             }
-            uint4 *dd = reinterpret_cast<uint4 *>(sr + x0);
+            uint4 *dd = reinterpret_cast<uint4 *>(sr + skw<kSkew>(x0));
             dd[0] = make_uint4(px[0], px[1], px[2], px[3]);
             dd[1] = make_uint4(px[4], px[5], px[6], px[7]);
           }
@@ -345,15 +370,15 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
     } else {
       if (raw_al16) {
         if (lane * 16 < W) {
-          stage16_raw(rp0, s0, lane * 16);
-          if (y + 1 < H) stage16_raw(rp1, s1, lane * 16);
+          stage16_raw<kSkew>(pf.r0, s0, lane * 16);
+          if (y + 1 < H) stage16_raw<kSkew>(pf.r1, s1, lane * 16);
         }
       } else {
         for (int r = 0; r < 2; ++r) {
           const int yy = y + r;
           if (yy >= H) break;
           const uint8_t *row = raw_cell + (int64_t)yy * W * 3;
-          for (int x0 = lane * 16; x0 < W; x0 += 1024) stage16_raw(load16_any(row, W, x0), r ? s1 : s0, x0);
+          for (int x0 = lane * 16; x0 < W; x0 += 1024) stage16_raw<kSkew>(load16_any(row, W, x0), r ? s1 : s0, x0);
         }
       }
     }
@@ -362,10 +387,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   int next_oy = 0;     // next output row of the band to finish
   int kv_base = -1;    // first band row cached in kv
   int slot = 0;        // ring slot of row y
-  fetch(ya0);
-  for (int y = ya0; y < yb; y += 2) {
-    stage(y);
-    if (y + 2 < yb) fetch(y + 2);
+  auto process = [&](int y) {
     wave_lds_fence();
     // horizontal taps: 7 (q, row) jobs of 64 output columns
     const int slot1 = slot + 1 == RING ? 0 : slot + 1;
@@ -374,13 +396,14 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
       const int q = job < 6 ? job >> 1 : 3;
       const int r = job < 6 ? (job & 1) : (lane >> 5);
       const int ox = q < 3 ? lane + 64 * q : 192 + (lane & 31);
-      const uint32_t *src = stg + (r ? g.spad : 0) + xm[q];
+      const uint32_t *rowp = stg + (r ? g.spad : 0);
       int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
         // Pillow weights are >= 0 and <= 2^22: 24-bit products (v_mul_u32_u24
-        // with SDWA byte selects), exact in 32 bits
-        const uint32_t v = src[t];
+        // with SDWA byte selects), exact in 32 bits. The window crosses at
+        // most one 32-pixel skew step (KS < 32), at tap xcr[q].
+        const uint32_t v = kSkew ? (rowp + (t < xcr[q] ? xsk[q] : xsk[q] + 4))[t] : rowp[xm[q] + t];
         const uint32_t kw = (uint32_t)wgt[q][t];
         a0 += (int32_t)__umul24(v & 255, kw);
         a1 += (int32_t)__umul24((v >> 8) & 255, kw);
@@ -444,6 +467,15 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
         }
       }
     }
+  };
+
+  // one row pair in flight while the previous one is computed (a second
+  // register set measured no faster and costs a wave per SIMD)
+  fetch(pa, ya0);
+  for (int y = ya0; y < yb; y += 2) {
+    stage(pa, y);
+    if (y + 2 < yb) fetch(pa, y + 2);
+    process(y);
   }
 }
 
@@ -457,8 +489,9 @@ static int wave_bytes4(const Geom4 &g) {
 
 static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g) {
   g.ks_v = resample_ksize_host(max_h, kOut);
-  g.ring = g.ks_v + 3;
-  g.spad = ((((max_w + 15) / 16) * 16 + ks_h + 16) + 3) & ~3;
+  g.ring = g.ks_v + 1; // an output row is finished within 2 rows of its window end
+  const int px = ((max_w + 15) / 16) * 16 + ks_h + 16;
+  g.spad = (px + ((px >> 5) << 2) + 4 + 3) & ~3; // skewed pixels (skw)
   g.wave_bytes = wave_bytes4(g);
   int nb = (waves_target + n - 1) / n;
   if (nb < 1) nb = 1;
