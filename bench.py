@@ -99,6 +99,9 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-images", type=int, default=3072)
+    ap.add_argument("--input", choices=("resident", "host"), default="resident",
+                    help="resident: cells already in HBM (value); host: Arrow RecordBatches in host "
+                         "memory through the pipelined to_tensor_fn (PCIe-inclusive, DESIGN.md §7)")
     ap.add_argument("--no-stage-events", action="store_true",
                     help="time without the per-stage HIP events (no roofline)")
     ap.add_argument("--depth", type=int, default=3,
@@ -145,10 +148,17 @@ def main():
         nb = 2  # two distinct resident batches, alternated
         batches = []
         cells_all = []
+        import pyarrow as pa
+
         for k in range(nb):
             cells, labels = make_cells(args.workload, B, seed=1000 * rank + k)
             cells_all += cells
-            batches.append(ldt_amd.ResidentBatch(cells, labels, device=dev))
+            if args.input == "host":
+                batches.append(pa.RecordBatch.from_arrays(
+                    [pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
+                    names=["image", "label"]))
+            else:
+                batches.append(ldt_amd.ResidentBatch(cells, labels, device=dev))
         px = [ldt_amd_dims(c) for c in cells_all[:B]]
         bytes_per_img = float(np.mean([h * w * 3 for (h, w) in px])) + OUT_BYTES
         comp_bytes = float(np.mean([len(c) for c in cells_all]))
@@ -224,11 +234,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded PIL-encoded JPEG cells resident in HBM; FOOD101 offline-unavailable)"
-                if args.workload != "c5" else "synthetic (uniform uint8 HWC generated in HBM)",
+        "data": (f"synthetic (seeded PIL-encoded JPEG cells {'resident in HBM' if args.input == 'resident' else 'in host Arrow RecordBatches, copied over PCIe every step'}; FOOD101 offline-unavailable)"
+                 if args.workload != "c5" else "synthetic (uniform uint8 HWC generated in HBM)"),
         "config": {"workload": f"{args.workload}: {wl['desc']}", "per_gpu_batch": B, "global_batch": B * world,
                    "parallelism": f"dp{world} (independent shards, no data-path collective)",
                    "pipeline_depth": 1 if args.workload == "c5" else args.depth,
+                   "input": "resident" if args.workload == "c5" else args.input,
                    "output": "float32[N,3,224,224] + int64[N] on device"},
         "roofline": {
             "kernel": "k_resize (fused chroma upsample + YCbCr->RGB + BILINEAR 224 + ToTensor store)"

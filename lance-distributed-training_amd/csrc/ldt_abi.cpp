@@ -14,10 +14,15 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -265,6 +270,77 @@ struct PinBuf {
   size_t cap = 0;
 };
 
+// Host copies into the pinned ring (Arrow cells -> pinned -> HBM) are the
+// host-side bottleneck of the PCIe path: one core moves ~6-10 GB/s. A small
+// persistent pool per context splits a large copy into chunks.
+class CopyPool {
+public:
+  explicit CopyPool(int nthreads) {
+    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this, i] { run(i + 1); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  void copy(void *dst, const void *src, size_t n) {
+    const int parts = (int)th_.size() + 1;
+    if (n < ((size_t)1 << 20) || th_.empty()) {
+      memcpy(dst, src, n);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      dst_ = static_cast<uint8_t *>(dst);
+      src_ = static_cast<const uint8_t *>(src);
+      n_ = n;
+      parts_ = parts;
+      pending_ = parts - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    part(0);
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return pending_ == 0; });
+  }
+
+private:
+  void part(int k) {
+    const size_t chunk = ((n_ + parts_ - 1) / parts_ + 63) & ~(size_t)63;
+    const size_t lo = std::min(n_, chunk * (size_t)k), hi = std::min(n_, lo + chunk);
+    if (hi > lo) memcpy(dst_ + lo, src_ + lo, hi - lo);
+  }
+  void run(int k) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+      }
+      part(k);
+      {
+        std::lock_guard<std::mutex> g(m_);
+        if (--pending_ == 0) done_cv_.notify_one();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  uint8_t *dst_ = nullptr;
+  const uint8_t *src_ = nullptr;
+  size_t n_ = 0;
+  int parts_ = 1, pending_ = 0;
+};
+
 struct ldt_ctx {
   int device = 0;
   std::string err;
@@ -276,6 +352,7 @@ struct ldt_ctx {
   int subseq_bits = 1024;
   DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_sub, d_pre, d_dscnt;
   bool coef_dirty = false; // a batch wrote coefficients but k_idct did not run
+  std::unique_ptr<CopyPool> copier; // host -> pinned copies (created on first use)
   static constexpr int kSlots = 2;
   PinBuf h_data[kSlots], h_plan[kSlots];
   hipEvent_t slot_ev[kSlots] = {nullptr, nullptr};
@@ -351,6 +428,16 @@ int ensure_dev(ldt_ctx *c, DevBuf &b, size_t need, hipStream_t s, bool zero = fa
   b.cap = cap;
   if (zero) HIPCHK(c, hipMemsetAsync(b.p, 0, cap, s));
   return LDT_OK;
+}
+
+void pinned_copy(ldt_ctx *c, void *dst, const void *src, size_t n) {
+  if (!c->copier) {
+    unsigned hw = std::thread::hardware_concurrency();
+    const char *e = getenv("LDT_COPY_THREADS");
+    int nt = e ? atoi(e) : (int)std::min(3u, hw > 1 ? hw - 1 : 0u);
+    c->copier.reset(new CopyPool(std::max(0, std::min(nt, 15))));
+  }
+  c->copier->copy(dst, src, n);
 }
 
 int ensure_pin(ldt_ctx *c, PinBuf &b, size_t need) {
@@ -755,7 +842,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if (!data_dev) {
     if ((rc = ensure_pin(c, c->h_data[sl], (size_t)total_bytes + 16))) return rc;
     if ((rc = ensure_dev(c, c->d_data, (size_t)total_bytes + 16, s))) return rc;
-    memcpy(c->h_data[sl].p, cells_host, (size_t)total_bytes);
+    pinned_copy(c, c->h_data[sl].p, cells_host, (size_t)total_bytes);
     HIPCHK(c, hipMemcpyAsync(c->d_data.p, c->h_data[sl].p, (size_t)total_bytes,
                              hipMemcpyHostToDevice, s));
     dev_cells = static_cast<const uint8_t *>(c->d_data.p);
@@ -1025,7 +1112,7 @@ int ldt_resize_raw(ldt_ctx *c, const uint8_t *hwc, int hwc_is_device, int64_t n,
     const size_t bytes = (size_t)(cell_stride * (n - 1) + (int64_t)h * w * 3);
     if ((rc = ensure_pin(c, c->h_data[sl], bytes))) return rc;
     if ((rc = ensure_dev(c, c->d_raw, bytes, s))) return rc;
-    memcpy(c->h_data[sl].p, hwc, bytes);
+    pinned_copy(c, c->h_data[sl].p, hwc, bytes);
     HIPCHK(c, hipMemcpyAsync(c->d_raw.p, c->h_data[sl].p, bytes, hipMemcpyHostToDevice, s));
     src = static_cast<const uint8_t *>(c->d_raw.p);
   }

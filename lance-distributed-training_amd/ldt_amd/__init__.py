@@ -13,6 +13,7 @@ from .dataset import (ArrowDataset, LanceDataset, SafeLanceDataset, dataset,  # 
                       get_safe_loader, write_dataset)
 from .sampler import FullScanSampler, ShardedBatchSampler, ShardedFragmentSampler  # noqa: F401
 from .transforms import (IMAGENET_MEAN, IMAGENET_STD, DecodePipeline, ResidentBatch, collate_fn,  # noqa: F401
-                         decode_arrow, decode_tensor_image, make_collate_fn, resize_raw)
+                         decode_arrow, decode_tensor_image, make_collate_fn, make_to_tensor_fn,
+                         resize_raw)
 
 __version__ = "0.1.0"

@@ -102,24 +102,31 @@ def _decoder(device) -> _Decoder:
 
 
 def decode_arrow(images: pa.Array, labels=None, *, device=None, normalize=None,
-                 stream: Optional[torch.cuda.Stream] = None):
+                 stream: Optional[torch.cuda.Stream] = None, ctx=None, out=None, out_lbl=None):
     """Decode an Arrow ``binary``/``large_binary`` array of JPEG cells.
 
     ``labels``: optional (address, offset, keepalive) as from ``_labels_buffer``
-    or an int64 sequence. Returns (image float32[N,3,224,224], label int64[N] or None).
+    or an int64 sequence. ``ctx``: a libldt context (default: the device's
+    shared one). Returns (image float32[N,3,224,224], label int64[N] or None).
+    The host cells are only borrowed for the call (copied into the context's
+    pinned ring, then sent to HBM on ``stream``).
     """
     if isinstance(images, pa.ChunkedArray):
         images = images.combine_chunks()
     dec = _decoder(device)
-    ctx = dec.ctx
+    ctx = ctx or dec.ctx
     n = len(images)
-    out = torch.empty((n, 3, _OUT, _OUT), dtype=torch.float32, device=dec.device)
+    if out is None:
+        out = torch.empty((n, 3, _OUT, _OUT), dtype=torch.float32, device=dec.device)
     lbl_keep = None
     if labels is not None and not isinstance(labels, tuple):
         arr = np.ascontiguousarray(np.asarray(labels, dtype=np.int64))
         lbl_keep = arr
         labels = (arr.ctypes.data, 0, arr)
-    out_lbl = torch.empty((n,), dtype=torch.int64, device=dec.device) if labels is not None else None
+    if labels is not None and out_lbl is None:
+        out_lbl = torch.empty((n,), dtype=torch.int64, device=dec.device)
+    elif labels is None:
+        out_lbl = None
     if n == 0:
         return out, out_lbl
     t = images.type
@@ -309,17 +316,30 @@ class DecodePipeline:
         self.sizes = [0] * self.depth
         self.k = 0
 
-    def decode(self, batch: "ResidentBatch", normalize=None):
+    def decode(self, batch, normalize=None, image_column: str = "image", label_column: str = "label"):
+        """Enqueue one batch: a ``ResidentBatch`` (cells already in HBM) or a
+        host ``pa.RecordBatch`` as LanceDataset yields it (its buffers are
+        copied into the slot's pinned ring during the call, then to HBM
+        asynchronously on the slot's stream)."""
         slot = self.k % self.depth
         self.k += 1
         s = self.streams[slot]
         cur = torch.cuda.current_stream(self.dec.device)
+        if isinstance(batch, ResidentBatch):
+            n, has_lbl = batch.n, batch.labels is not None
+        else:
+            images = _column(batch, image_column)
+            lab = _labels_buffer(batch, label_column)
+            n, has_lbl = len(images), lab is not None
         with torch.cuda.stream(s):
-            out = torch.empty((batch.n, 3, _OUT, _OUT), dtype=torch.float32, device=self.dec.device)
-            lbl = (torch.empty((batch.n,), dtype=torch.int64, device=self.dec.device)
-                   if batch.labels is not None else None)
-        batch.decode(out, lbl, normalize, ctx=self.ctxs[slot], stream=s)
-        self.sizes[slot] = batch.n
+            out = torch.empty((n, 3, _OUT, _OUT), dtype=torch.float32, device=self.dec.device)
+            lbl = torch.empty((n,), dtype=torch.int64, device=self.dec.device) if has_lbl else None
+        if isinstance(batch, ResidentBatch):
+            batch.decode(out, lbl, normalize, ctx=self.ctxs[slot], stream=s)
+        else:
+            decode_arrow(images, lab, device=self.dec.device, normalize=normalize, stream=s,
+                         ctx=self.ctxs[slot], out=out, out_lbl=lbl)
+        self.sizes[slot] = n
         cur.wait_stream(s)
         out.record_stream(cur)
         if lbl is not None:
@@ -334,15 +354,52 @@ class DecodePipeline:
                 tot[k] = (a[0] + ms, a[1] + n)
         return tot
 
-    def check(self):
-        bad = {}
-        for c, s, n in zip(self.ctxs, self.streams, self.sizes):
-            if n == 0:
-                continue
-            st = np.zeros(n, np.int32)
-            rc = c.lib.ldt_fetch_status(c.handle, s.cuda_stream, st.ctypes.data, n)
-            if rc != _lib.LDT_ERR_IMAGE:
-                c.check(rc, "ldt_fetch_status")
-            bad.update({int(i): int(st[i]) for i in np.nonzero(st)[0]})
+    def _slot_status(self, i: int) -> dict:
+        c, s, n = self.ctxs[i], self.streams[i], self.sizes[i]
+        if n == 0:
+            return {}
+        st = np.zeros(n, np.int32)
+        rc = c.lib.ldt_fetch_status(c.handle, s.cuda_stream, st.ctypes.data, n)
+        if rc != _lib.LDT_ERR_IMAGE:
+            c.check(rc, "ldt_fetch_status")
+        return {int(j): int(st[j]) for j in np.nonzero(st)[0]}
+
+    def check_slot(self, i: int):
+        """Wait for slot i's most recent batch; raise ImageDecodeError on failures."""
+        bad = self._slot_status(i)
+        self.sizes[i] = 0
         if bad:
             raise ImageDecodeError(bad)
+
+    def check(self):
+        bad = {}
+        for i in range(self.depth):
+            bad.update(self._slot_status(i))
+        if bad:
+            raise ImageDecodeError(bad)
+
+
+def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, **fixed):
+    """A pipelined ``to_tensor_fn`` for ``LanceDataset(..., to_tensor_fn=...)``
+    (lance_iterable.py:53-59): each call enqueues its RecordBatch on one of
+    `depth` contexts/streams and returns at once, so batch k+1's host copy and
+    kernels overlap batch k's. The tensors are ready on torch's current stream
+    (it waits for the slot's stream). Per-image errors are reported
+    asynchronously: by ``fn.check()``, and at the latest when a slot is reused
+    (`depth` calls later) — unlike the synchronous ``decode_tensor_image``."""
+    pipe = DecodePipeline(depth=depth, device=device)
+
+    def to_tensor_fn(batch, **kwargs):
+        if pipe.k >= pipe.depth:
+            pipe.check_slot(pipe.k % pipe.depth)
+        img, lbl = pipe.decode(batch, normalize=kwargs.get("normalize", normalize),
+                               image_column=kwargs.get("image_column", fixed.get("image_column", "image")),
+                               label_column=kwargs.get("label_column", fixed.get("label_column", "label")))
+        out = {"image": img}
+        if lbl is not None:
+            out["label"] = lbl
+        return out
+
+    to_tensor_fn.check = pipe.check
+    to_tensor_fn.pipeline = pipe
+    return to_tensor_fn

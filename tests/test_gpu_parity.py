@@ -371,3 +371,33 @@ def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
     img = ldt_amd.decode_tensor_image(_batch(nxt))["image"].cpu().numpy()
     for k in range(3):
         _check(img[k], oracle.jpeg_to_tensor(nxt[k]), f"after-error[{k}]")
+
+
+def test_pipelined_to_tensor_fn_host_batches():
+    """make_to_tensor_fn: host RecordBatches (as LanceDataset yields them)
+    decoded 3 in flight; results match the oracle in order, and a bad row is
+    reported by check() with its row index."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import synth
+
+    fn = ldt_amd.make_to_tensor_fn(depth=3)
+    batches = []
+    for k in range(5):
+        cells, labels = synth.food101_like(12, seed=40 + k)
+        batches.append((cells, labels, _batch(cells, labels)))
+    outs = [fn(rb, unknown_kwarg=1) for _, _, rb in batches]
+    fn.check()
+    torch.cuda.synchronize()
+    for (cells, labels, _), o in zip(batches, outs):
+        assert np.array_equal(o["label"].cpu().numpy(), labels)
+        img = o["image"].cpu().numpy()
+        for k in (0, 5, 11):
+            _check(img[k], oracle.jpeg_to_tensor(cells[k]), "pipelined")
+    bad = read_golden("jpeg/bad_truncated.bin")
+    good = synth.encode(synth.field(64, 80, 3))
+    fn(_batch([good, bad, good]))
+    with pytest.raises(ldt_amd.ImageDecodeError) as ei:
+        fn.check()
+    assert set(ei.value.rows) == {1}
