@@ -739,6 +739,9 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
         sbits = (bits + k * (kSlotsPerWg - 1) - 1) / (k * (kSlotsPerWg - 1));
         sbits = std::min<int64_t>(SB, std::max<int64_t>(256, (sbits + 31) & ~(int64_t)31));
       }
+      // an odd number of 32-bit words per range: lanes' LDS window reads start
+      // in distinct banks (the window is not skewed)
+      if (((sbits >> 5) & 1) == 0 && sbits >= 256) sbits = sbits + 32 <= SB ? sbits + 32 : sbits - 32;
       d.sub_bits = (int32_t)sbits;
       // subsequence slots: sum over segments of ceil(bits_s / S) <= bits / S + nseg
       const int64_t slots = (d.src_len * 8 + sbits - 1) / sbits + d.nseg;

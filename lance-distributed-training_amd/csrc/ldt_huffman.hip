@@ -54,13 +54,13 @@ extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
 // followed by kSegPad zero bytes, and a symbol starting before the segment end
 // reads at most 31 bits from its start.
 // ---------------------------------------------------------------------------
-// The LDS window is skewed by one word per 32 (word i at i + i/32): lanes'
-// ranges start S/8 bytes apart, which would otherwise map every lane to the
-// same few banks.
-__device__ __forceinline__ int32_t skew(int32_t i) { return i + (i >> 5); }
+// The LDS window is stored linearly. Lanes' ranges start S/32 words apart, and
+// the planner keeps S/32 odd, so lanes at the same relative position fall in
+// distinct banks without a skew (which would cost 3 VALU per symbol on the
+// refill address).
 struct LdsWords {
   lds_cu32 w;
-  __device__ __forceinline__ uint32_t operator()(int32_t i) const { return w[skew(i)]; }
+  __device__ __forceinline__ uint32_t operator()(int32_t i) const { return w[i]; }
 };
 struct GlobWords {
   const uint32_t *w; // 4-aligned
@@ -476,7 +476,7 @@ hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
 // only counts blocks per range; k_huff_write then decodes every range from its
 // true entry and k_dc_scan adds the DC predictors.
 //
-// LDS window: the workgroup's destuffed bytes, byte-swapped and skewed. Without
+// LDS window: the workgroup's destuffed bytes, byte-swapped. Without
 // restart markers they span 256 * S/8 + 76 bytes; a workgroup whose ranges
 // span more (many small restart segments, kSegPad apart) reads global memory
 // instead. LDS per workgroup stays under a third of the CU's 160 KB at S = 1024
@@ -485,8 +485,8 @@ hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
 
 __host__ __device__ inline int window_bytes(int S) { return 256 * (S / 8) + 128; }
 __host__ __device__ inline int window_lds_bytes(int S) {
-  const int words = window_bytes(S) / 4;
-  return ((words + words / 32 + 1) * 4 + 15) & ~15;
+  const int words = window_bytes(S) / 4 + 1;
+  return (words * 4 + 15) & ~15;
 }
 
 // Locate the segment that owns image-local slot `lt` (sub_first ascending).
@@ -576,7 +576,7 @@ __device__ __forceinline__ Dec sub_setup(const ImgDesc &d, const Segment *__rest
   sc.in_lds = nbytes <= window_bytes(Smax);
   sc.gw = reinterpret_cast<const uint32_t *>(dstuf + wb);
   if (sc.in_lds)
-    for (int i = tid; i < (int)nbytes / 4; i += kSyncThreads) win[skew(i)] = __builtin_bswap32(sc.gw[i]);
+    for (int i = tid; i < (int)nbytes / 4; i += kSyncThreads) win[i] = __builtin_bswap32(sc.gw[i]);
   sc.pbias = (int32_t)(seg0 - wb) * 8;
   __syncthreads();
   return dec;
