@@ -67,14 +67,15 @@ struct GlobWords {
   __device__ __forceinline__ uint32_t operator()(int32_t i) const { return __builtin_bswap32(w[i]); }
 };
 
-// Reader state: words wi-2 (hi), wi-1 (lo) and wi (nxt, prefetched); o bits
-// of hi are consumed, 1 <= o <= 32, so the next 32 bits are one alignbit.
+// Reader state: words wi-2 (hi), wi-1 (lo) and wi (nxt, prefetched); rs is
+// 32 minus the consumed bits of hi (0 <= rs <= 31), so the next 32 bits are
+// one alignbit with rs as its shift.
 template <class W>
 struct Rd {
   W src;
   uint32_t hi, lo, nxt;
   int32_t wi;
-  int32_t o;
+  int32_t rs;
   int32_t p;     // source bit position of the next symbol
   __device__ __forceinline__ void seek(int32_t q) {
     const int32_t i = (q - 1) >> 5;
@@ -82,22 +83,22 @@ struct Rd {
     lo = src(i + 1);
     nxt = src(i + 2);
     wi = i + 2;
-    o = q - 32 * i;
+    rs = 32 * (i + 1) - q;
     p = q;
     // settle the seek's loads here: the decode loop's header then inherits no
     // pending LDS load and waits only on its own lookup (lgkmcnt(0))
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
   __device__ __forceinline__ uint32_t peek() const {
-    return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)(32 - o));
+    return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)rs);
   }
   __device__ __forceinline__ void consume(int t) { // t <= 31
     p += t;
-    o += t;
-    const bool m = o > 32;
+    rs -= t;
+    const bool m = rs < 0;
     hi = m ? lo : hi;
     lo = m ? nxt : lo;
-    o = m ? o - 32 : o;
+    rs = m ? rs + 32 : rs;
     wi += m ? 1 : 0;
     nxt = src(wi);
   }
