@@ -558,6 +558,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   int32_t n_chunks = 0;          // destuff chunks (kDsChunk bytes of scan data each)
   std::vector<int32_t> chunk_img;
   int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3, max_tabs = 1;
+  int max_sub_bits = 64; // largest per-image S: sizes the decoders' LDS window
   bool any_bad = false;
   for (int64_t i = 0; i < n; ++i) {
     ImgPlan &ip = P[(size_t)i];
@@ -743,6 +744,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       // in distinct banks (the window is not skewed)
       if (((sbits >> 5) & 1) == 0 && sbits >= 256) sbits = sbits + 32 <= SB ? sbits + 32 : sbits - 32;
       d.sub_bits = (int32_t)sbits;
+      if (sbits > max_sub_bits) max_sub_bits = (int)sbits;
       // subsequence slots: sum over segments of ceil(bits_s / S) <= bits / S + nseg
       const int64_t slots = (d.src_len * 8 + sbits - 1) / sbits + d.nseg;
       d.wg_count = (int32_t)((slots + kSlotsPerWg - 1) / kSlotsPerWg);
@@ -870,7 +872,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.max_w = max_w;
   p.max_h = max_h;
   p.max_blocks = max_blocks;
-  p.subseq_bits = parallel ? SB : 0;
+  p.subseq_bits = parallel ? max_sub_bits : 0;
   p.warm_pct = c->warm_pct;
   p.n_wg = parallel ? n_wg : 0;
   p.wg_img = reinterpret_cast<const int32_t *>(dp + off_wg);
