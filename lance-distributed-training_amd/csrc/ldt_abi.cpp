@@ -557,7 +557,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   std::vector<int32_t> wg_img;
   int32_t n_chunks = 0;          // destuff chunks (kDsChunk bytes of scan data each)
   std::vector<int32_t> chunk_img;
-  int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3, max_tabs = 1;
+  int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3, max_tabs = 1, n_fast420 = 0;
   int max_sub_bits = 64; // largest per-image S: sizes the decoders' LDS window
   bool any_bad = false;
   for (int64_t i = 0; i < n; ++i) {
@@ -764,6 +764,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     const int64_t nblk = nmcu * d.bpm;
     coef_blocks += nblk;
     if (nblk > max_blocks) max_blocks = nblk;
+    if (resize_fast420(d)) ++n_fast420;
     if (H.width > max_w) max_w = H.width;
     if (H.height > max_h) max_h = H.height;
     int kh = resample_ksize_host(H.width, kOut), kv = resample_ksize_host(H.height, kOut);
@@ -880,6 +881,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
   p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
   p.max_tabs = max_tabs;
+  p.n_fast420 = n_fast420;
   c->last_off_redo = off_redo;
   DevWork w;
   w.data = dev_cells;

@@ -36,6 +36,7 @@ struct DevPlan {
   const int32_t *wg_img; // workgroup -> image
   int32_t *redo;         // set when a workgroup-boundary walk did not converge
   int max_tabs;          // max distinct Huffman tables of one image (LDS slots)
+  int n_fast420;         // images on k_resize4's fast staging path (resize_fast420)
   // destuff chunks (4 KB of entropy-coded bytes each)
   int n_chunks;
   const int32_t *chunk_img; // chunk -> image

@@ -152,6 +152,12 @@ struct Geom4 {
 
 constexpr int kKvRows = 16; // vertical coefficient rows cached per wave
 
+// SRC: 0 JPEG planes, 4:2:0 fast staging (resize_fast420 images only);
+// 2 JPEG planes, generic staging (the other images); 1 raw HWC rows, 16-byte
+// aligned; 3 raw HWC rows, any alignment. Each variant is its own kernel so
+// the waitcnt pass never sees another path's loads pending at the loop's
+// merge points (that forced a vmcnt(0) ahead of the horizontal taps and
+// serialised the prefetch).
 template <int SRC, int KS>
 __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ descs,
                                                  const uint8_t *__restrict__ planes, RawSrc raw,
@@ -164,17 +170,19 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   // Skewed staging for raw rows (c5: 4-5-way tap conflicts otherwise, and the
   // kernel is LDS-bound). JPEG rows stay plain: the skew's extra registers
   // cost a wave per SIMD there, which is worth more than its 2-way conflicts.
-  constexpr bool kSkew = SRC == 1;
+  constexpr bool kJpeg = SRC == 0 || SRC == 2;
+  constexpr bool kSkew = !kJpeg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
   for (int i = tid; i < 768; i += 256) s_lut[i] = lut[i];
   __syncthreads(); // the only workgroup barrier
-  const int task = blockIdx.x * 4 + wave;
+  // wave-uniform task: descriptor loads become scalar loads into SGPRs
+  const int task = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wave);
   if (task >= g.ntask) return;
   const int img = task / g.nbands, band = task - img * g.nbands;
-  if (SRC == 0 && status[img] != 0) return;
+  if (kJpeg && (status[img] != 0 || resize_fast420(descs[img]) != (SRC == 0))) return;
   int W, H;
-  if constexpr (SRC == 0) {
+  if constexpr (kJpeg) {
     W = descs[img].width;
     H = descs[img].height;
   } else {
@@ -223,7 +231,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
     ya = ymin_a;
     yb = ymin_b + cnt_b;
   }
-  const int ya0 = SRC == 0 ? (ya & ~1) : ya;
+  const int ya0 = kJpeg ? (ya & ~1) : ya;
 
   // vertical-pass items: 168 dwords (3 channels x 56 groups of 4 columns)
   int vc[3], vo[3];
@@ -235,23 +243,29 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   }
 
   // JPEG fast path: 4:2:0 with both chroma planes fancy-upsampled, W <= 512
-  bool fast420 = false;
+  constexpr bool fast420 = SRC == 0;
   int rc = 5, cdh = 1;
+  // plane geometry copied to registers once: the wave fences in process()
+  // would otherwise make every fetch reload it (a dependent global round trip
+  // per plane load, which serialised the prefetch)
+  int64_t po0 = 0, po1 = 0, po2 = 0;
+  int ps0 = 0, ps1 = 0;
   const ImgDesc *dp = nullptr;
   const uint8_t *raw_cell = nullptr;
-  bool raw_al16 = false;
-  if constexpr (SRC == 0) {
+  constexpr bool raw_al16 = SRC == 1;
+  if constexpr (kJpeg) {
     dp = descs + img;
     const ImgDesc &d = *dp;
-    fast420 = d.color == 0 && d.hf[1] == 2 && d.vf[1] == 2 && d.hf[2] == 2 && d.vf[2] == 2 &&
-              d.cdw[1] > 2 && d.cdw[2] > 2 && d.cdw[1] == d.cdw[2] && d.cdh[1] == d.cdh[2] &&
-              d.plane_stride[1] == d.plane_stride[2] && W <= 512;
     const int dw = d.cdw[1];
     rc = lane == (dw - 1) / 4 ? (dw - 1) % 4 + 1 : 5;
     cdh = d.cdh[1];
+    po0 = d.plane_off[0];
+    po1 = d.plane_off[1];
+    po2 = d.plane_off[2];
+    ps0 = d.plane_stride[0];
+    ps1 = d.plane_stride[1];
   } else {
     raw_cell = raw.base + (int64_t)img * raw.cell_stride;
-    raw_al16 = ((((uintptr_t)raw_cell) & 15) == 0) && ((W * 3) & 15) == 0 && W <= 1024;
   }
 
   // ---- prefetch helpers ----
@@ -261,14 +275,12 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   } pa;
   auto fetch = [&](Pre &pf, int y) {
     Jpair &jp = pf.jp;
-    if constexpr (SRC == 0) {
-      if (fast420) {
-        const ImgDesc &d = *dp;
+    if constexpr (kJpeg) {
+      if constexpr (fast420) {
         const int x0 = lane * 8;
-        const uint8_t *py = planes + d.plane_off[0] + (int64_t)y * d.plane_stride[0] + x0;
+        const uint8_t *py = planes + po0 + (int64_t)y * ps0 + x0;
         jp.y0 = x0 < W ? *reinterpret_cast<const uint2 *>(py) : make_uint2(0, 0);
-        jp.y1 = (x0 < W && y + 1 < H) ? *reinterpret_cast<const uint2 *>(py + d.plane_stride[0])
-                                     : make_uint2(0, 0);
+        jp.y1 = (x0 < W && y + 1 < H) ? *reinterpret_cast<const uint2 *>(py + ps0) : make_uint2(0, 0);
         const int cy = y >> 1;
         const int rows[3] = {max(cy - 1, 0), cy, min(cy + 1, cdh - 1)};
         const int cx0 = lane * 4;
@@ -276,13 +288,12 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
         for (int c = 0; c < 2; ++c)
 #pragma unroll
           for (int r = 0; r < 3; ++r)
-            jp.c[c][r] = cx0 < d.plane_stride[1]
-                             ? *reinterpret_cast<const uint32_t *>(planes + d.plane_off[1 + c] +
-                                                                   (int64_t)rows[r] * d.plane_stride[1] + cx0)
-                             : 0u;
+            jp.c[c][r] = cx0 < ps1 ? *reinterpret_cast<const uint32_t *>(planes + (c ? po2 : po1) +
+                                                                         (int64_t)rows[r] * ps1 + cx0)
+                                   : 0u;
       }
     } else {
-      if (raw_al16) {
+      if constexpr (raw_al16) {
         const int x0 = lane * 16;
         if (x0 < W) {
           pf.r0 = load16_aligned(raw_cell + (int64_t)y * W * 3 + 3 * x0);
@@ -296,9 +307,9 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   auto stage = [&](const Pre &pf, int y) {
     const Jpair &jp = pf.jp;
     uint32_t *s0 = stg, *s1 = stg + g.spad;
-    if constexpr (SRC == 0) {
+    if constexpr (kJpeg) {
       const ImgDesc &d = *dp;
-      if (fast420) {
+      if constexpr (fast420) {
         const int x0 = lane * 8;
         int cb[2][8], crr[2][8];
 #pragma unroll
@@ -368,7 +379,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
         }
       }
     } else {
-      if (raw_al16) {
+      if constexpr (raw_al16) {
         if (lane * 16 < W) {
           stage16_raw<kSkew>(pf.r0, s0, lane * 16);
           if (y + 1 < H) stage16_raw<kSkew>(pf.r1, s1, lane * 16);
@@ -553,7 +564,15 @@ bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t
   if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g)) return false;
   if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g), g)) return false;
   RawSrc raw{nullptr, 0, 0, 0};
-  return dispatch4<0>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s,
+  // fast-path images and the rest go to separate kernels (each skips the
+  // other's images); a batch of one kind launches one kernel
+  if (p.n_fast420 > 0) {
+    if (!dispatch4<0>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s,
+                      err))
+      return false;
+    if (*err != hipSuccess || p.n_fast420 == p.n) return true;
+  }
+  return dispatch4<2>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s,
                       err);
 }
 
@@ -565,6 +584,12 @@ bool launch_resize4_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, i
   if (!make_geom4(n, wd, h, ks_h, 1, g)) return false;
   if (!make_geom4(n, wd, h, ks_h, waves_target4(g), g)) return false;
   RawSrc raw{hwc, cell_stride, h, wd};
+  const bool al16 = (((uintptr_t)hwc) & 15) == 0 && (cell_stride & 15) == 0 && ((wd * 3) & 15) == 0 &&
+                    wd <= 1024;
+  if (!al16)
+    return dispatch4<3>(ks_h, (const ImgDesc *)nullptr, (const uint8_t *)nullptr, raw, lut,
+                        (const int64_t *)nullptr, out, (int64_t *)nullptr, (const int32_t *)nullptr, g,
+                        s, err);
   return dispatch4<1>(ks_h, (const ImgDesc *)nullptr, (const uint8_t *)nullptr, raw, lut,
                       (const int64_t *)nullptr, out, (int64_t *)nullptr, (const int32_t *)nullptr, g,
                       s, err);

@@ -44,6 +44,15 @@ struct ImgDesc {
   int32_t sub_bits;  // parallel Huffman subsequence length S of this image (bits)
 };
 
+// k_resize4's fast staging path: 4:2:0 YCbCr with both chroma planes
+// fancy-upsampled (h2v2), one lane per 8 luma columns (W <= 512). Shared by
+// the host dispatch and the kernel so both agree image by image.
+__host__ __device__ inline bool resize_fast420(const ImgDesc &d) {
+  return d.color == 0 && d.hf[1] == 2 && d.vf[1] == 2 && d.hf[2] == 2 && d.vf[2] == 2 &&
+         d.cdw[1] > 2 && d.cdw[2] > 2 && d.cdw[1] == d.cdw[2] && d.cdh[1] == d.cdh[2] &&
+         d.plane_stride[1] == d.plane_stride[2] && d.width <= 512;
+}
+
 // One entropy-coded segment (a restart interval, or the whole scan).
 struct Segment {
   int32_t img;

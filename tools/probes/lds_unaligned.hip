@@ -1,0 +1,31 @@
+// Probe: does ds_read_b32 at an unaligned LDS byte address return the 4 bytes
+// starting there (gfx950)? Writes bytes 0..255 to LDS, reads dwords at byte
+// offsets 0..15 with inline-asm ds_read_b32 and stores them.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+__global__ void k(uint32_t *out) {
+  __shared__ uint8_t s[256];
+  int t = threadIdx.x;
+  s[t] = (uint8_t)t;
+  __syncthreads();
+  if (t < 16) {
+    uint32_t v;
+    uint32_t addr = (uint32_t)(uintptr_t)(&s[0]) + t;
+    asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    out[t] = v;
+  }
+}
+int main() {
+  uint32_t *d, h[16];
+  hipMalloc(&d, 64);
+  hipLaunchKernelGGL(k, dim3(1), dim3(256), 0, 0, d);
+  hipMemcpy(h, d, 64, hipMemcpyDeviceToHost);
+  int ok = 1;
+  for (int i = 0; i < 16; ++i) {
+    uint32_t e = (uint32_t)i | ((uint32_t)(i + 1) << 8) | ((uint32_t)(i + 2) << 16) | ((uint32_t)(i + 3) << 24);
+    printf("off %2d: %08x (unaligned-correct %08x)%s\n", i, h[i], e, h[i] == e ? "" : "  <-- differs");
+    if (h[i] != e) ok = 0;
+  }
+  printf(ok ? "UNALIGNED OK\n" : "UNALIGNED NOT SUPPORTED\n");
+  return 0;
+}
