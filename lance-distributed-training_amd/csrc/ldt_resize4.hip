@@ -398,9 +398,9 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   int next_oy = 0;     // next output row of the band to finish
   int kv_base = -1;    // first band row cached in kv
   int slot = 0;        // ring slot of row y
-  auto process = [&](int y) {
-    wave_lds_fence();
-    // horizontal taps: 7 (q, row) jobs of 64 output columns
+  // horizontal taps of the staged row pair y, y+1: 7 (q, row) jobs of 64
+  // output columns
+  auto horizontal = [&](int y) {
     const int slot1 = slot + 1 == RING ? 0 : slot + 1;
 #pragma unroll
     for (int job = 0; job < 7; ++job) {
@@ -427,9 +427,9 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
       rw[2 * RING * kOut] = (uint8_t)min((uint32_t)a2 >> kPrecisionBits, 255u);
     }
     slot = slot1 + 1 == RING ? 0 : slot1 + 1;
-    wave_lds_fence();
-    // finish every output row whose vertical window is complete
-    const int done = y + 2; // rows [ya0, done) are in the ring
+  };
+  // finish every output row whose vertical window lies in ring rows [ya0, done)
+  auto vertical = [&](int done) {
     while (next_oy < nb) {
       const int j = next_oy;
       if (j >= kv_base + kKvRows || kv_base < 0) {
@@ -480,14 +480,23 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
     }
   };
 
-  // one row pair in flight while the previous one is computed (a second
-  // register set measured no faster and costs a wave per SIMD)
+  // One row pair in flight while the previous one is computed (a second
+  // register set measured no faster and costs a wave per SIMD). The output
+  // rows completed by the previous pair are finished BEFORE this pair's
+  // horizontal taps: their float4 stores then drain behind the taps instead
+  // of being waited for (vmcnt counts loads and stores together) by the next
+  // staging's wait for its prefetched rows. The ring size is unchanged: the
+  // rows still pending need at most ks_v - 1 earlier rows plus this pair.
   fetch(pa, ya0);
   for (int y = ya0; y < yb; y += 2) {
     stage(pa, y);
     if (y + 2 < yb) fetch(pa, y + 2);
-    process(y);
+    wave_lds_fence();
+    vertical(y);
+    horizontal(y);
+    wave_lds_fence();
   }
+  vertical(yb + 1);
 }
 
 // ---------------------------------------------------------------------------
