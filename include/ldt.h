@@ -69,6 +69,9 @@ extern "C" {
                                  0: every image uses LDT_OPT_SUBSEQ_BITS        */
 #define LDT_OPT_SYNC_WARM 7   /* parallel decoder phase 1 starts this % of S
                                  before each range (0..200, default 0)         */
+#define LDT_OPT_DEBUG_SKIP 8  /* measurement only: bit 0 skips the resize
+                                 launch, bit 1 the IDCT launch (outputs are
+                                 then WRONG; marginal-cost experiments)         */
 
 /* ---- stages reported by ldt_stage_times ---- */
 #define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */

@@ -349,6 +349,7 @@ struct ldt_ctx {
   int resize_impl = 0;
   bool subseq_fit = true;
   int warm_pct = 0;
+  int debug_skip = 0; // LDT_OPT_DEBUG_SKIP
   int subseq_bits = 1024;
   DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_sub, d_pre, d_dscnt;
   bool coef_dirty = false; // a batch wrote coefficients but k_idct did not run
@@ -901,12 +902,13 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   else HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_dc_scan(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
-  HIPCHK(c, launch_idct(p, w, s));
+  if (!(c->debug_skip & 2)) HIPCHK(c, launch_idct(p, w, s));
   c->coef_dirty = false;
   prof_mark(c, LDT_STAGE_IDCT, s);
   {
     hipError_t rerr = hipSuccess;
-    if (!(c->resize_impl != 2 &&
+    if (c->debug_skip & 1) {
+    } else if (!(c->resize_impl != 2 &&
           launch_resize4_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr)) &&
         !launch_resize2_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr))
       rerr = launch_resize_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s);
@@ -1010,6 +1012,9 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
   case LDT_OPT_SYNC_WARM:
     if (value < 0 || value > 200) return set_err(c, LDT_ERR_ARG, "sync warm-up %lld", (long long)value);
     c->warm_pct = (int)value;
+    return LDT_OK;
+  case LDT_OPT_DEBUG_SKIP:
+    c->debug_skip = (int)value;
     return LDT_OK;
   case LDT_OPT_SUBSEQ_FIT:
     c->subseq_fit = value != 0;
@@ -1129,7 +1134,8 @@ int ldt_resize_raw(ldt_ctx *c, const uint8_t *hwc, int hwc_is_device, int64_t n,
   prof_begin(c, LDT_STAGE_RESIZE, s);
   {
     hipError_t rerr = hipSuccess;
-    if (!(c->resize_impl != 2 &&
+    if (c->debug_skip & 1) {
+    } else if (!(c->resize_impl != 2 &&
           launch_resize4_raw(src, cell_stride, (int)n, h, w, static_cast<const float *>(c->d_plan.p),
                              out_img_dev, s, &rerr)) &&
         !launch_resize2_raw(src, cell_stride, (int)n, h, w, static_cast<const float *>(c->d_plan.p),
