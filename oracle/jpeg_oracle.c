@@ -11,6 +11,8 @@
  *       Image.open(io.BytesIO(b)).convert("RGB")
  *       -> Pillow 12.2.0 JpegDecode -> libjpeg-turbo 3.1.4.1 defaults:
  *          jdhuff.c   (baseline Huffman decode, DC prediction, restart markers)
+ *          jdphuff.c  (progressive SOF2: DC/AC first and refinement scans,
+ *                      EOB runs; jdcoefct.c buffers all scans, then one IDCT)
  *          jidctint.c (JDCT_ISLOW, CONST_BITS 13, PASS1_BITS 2, range-limit table)
  *          jdsample.c (h2v2 / h2v1 fancy upsampling, box when width <= 2)
  *          jdmainct.c (context rows: replicated first/last chroma rows)
@@ -39,7 +41,7 @@
 
 #define ORC_OK 0
 #define ORC_ERR_FORMAT -1      /* not a JPEG / malformed marker structure */
-#define ORC_ERR_UNSUPPORTED -2 /* progressive, arithmetic, 12-bit, CMYK ... */
+#define ORC_ERR_UNSUPPORTED -2 /* arithmetic, lossless, 12-bit, CMYK ...    */
 #define ORC_ERR_TRUNCATED -3   /* entropy data ends before the last MCU     */
 #define ORC_ERR_NOMEM -4
 
@@ -75,6 +77,8 @@ typedef struct {
   const uint8_t *scan;   /* first byte of entropy-coded data */
   const uint8_t *end;
   int scan_ncomp, scan_comp[4];
+  int progressive;       /* SOF2 */
+  const uint8_t *sos;    /* progressive: the first SOS marker (FF DA) */
 } orc_jpeg;
 
 /* jpeg_natural_order (jutils.c): zigzag index -> natural index */
@@ -126,7 +130,8 @@ static int orc_parse(const uint8_t *d, size_t len, orc_jpeg *j) {
     if (L < 2 || p + L > e) return ORC_ERR_FORMAT;
     const uint8_t *s = p + 2, *se = p + L;
     switch (m) {
-    case 0xC0: case 0xC1: { /* SOF0 baseline / SOF1 extended Huffman */
+    case 0xC0: case 0xC1: case 0xC2: { /* SOF0 baseline / SOF1 extended / SOF2 progressive */
+      j->progressive = m == 0xC2;
       if (se - s < 6) return ORC_ERR_FORMAT;
       if (s[0] != 8) return ORC_ERR_UNSUPPORTED; /* 12-bit */
       j->height = rd16(s + 1);
@@ -147,7 +152,7 @@ static int orc_parse(const uint8_t *d, size_t len, orc_jpeg *j) {
       have_sof = 1;
       break;
     }
-    case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9:
+    case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9:
     case 0xCA: case 0xCB: case 0xCD: case 0xCE: case 0xCF:
       return ORC_ERR_UNSUPPORTED; /* progressive / lossless / arithmetic */
     case 0xC4: { /* DHT */
@@ -198,6 +203,11 @@ static int orc_parse(const uint8_t *d, size_t len, orc_jpeg *j) {
       break;
     case 0xDA: { /* SOS */
       if (!have_sof) return ORC_ERR_FORMAT;
+      if (j->progressive) { /* every scan is parsed by orc_decode_prog */
+        j->sos = p - 2;
+        j->end = e;
+        return ORC_OK;
+      }
       int ns = s[0];
       if (ns < 1 || ns > 4 || se - s < 1 + 2 * ns + 3) return ORC_ERR_FORMAT;
       j->scan_ncomp = ns;
@@ -473,6 +483,254 @@ static void orc_idct_islow(const int16_t *coef, const uint16_t *q, uint8_t *out,
 }
 
 /* ------------------------------------------------------------------------ */
+/* Progressive decode (SOF2): jdphuff.c restated. Every scan updates one      */
+/* coefficient array per component (jdcoefct.c full-image buffer); the IDCT  */
+/* runs once after the last scan. Block smoothing (jdcoefct.c                */
+/* decompress_smooth_data) only applies while coefficients 1..9 are not      */
+/* fully refined; such files are reported unsupported.                       */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+  int16_t *coef[4];        /* per component: bw*bh blocks x 64, natural order */
+  int coef_bits[4][64];    /* jdphuff.c cinfo->coef_bits: Al of the last scan, -1 never */
+} orc_prog;
+
+/* One AC refinement correction bit on an already-nonzero coefficient. */
+static void orc_refine_bit(orc_br *b, int16_t *c, int p1, int m1) {
+  if (orc_get(b, 1)) {
+    if ((*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
+  }
+}
+
+/* One scan: header at sos (FF DA), entropy data after it. Returns the first
+ * byte after the scan's data (the next marker) or NULL on error. */
+static const uint8_t *orc_prog_scan(orc_jpeg *j, orc_prog *pg, const uint8_t *sos, int *err) {
+  const uint8_t *e = j->end;
+  if (sos + 4 > e) { *err = ORC_ERR_FORMAT; return NULL; }
+  int L = rd16(sos + 2);
+  const uint8_t *s = sos + 4, *se = sos + 2 + L;
+  if (L < 2 || se > e) { *err = ORC_ERR_FORMAT; return NULL; }
+  int ns = s[0];
+  if (ns < 1 || ns > 4 || se - s < 1 + 2 * ns + 3) { *err = ORC_ERR_FORMAT; return NULL; }
+  int comp[4];
+  for (int i = 0; i < ns; i++) {
+    int cid = s[1 + 2 * i], ci = -1;
+    for (int c = 0; c < j->ncomp; c++)
+      if (j->comp[c].id == cid) ci = c;
+    if (ci < 0) { *err = ORC_ERR_FORMAT; return NULL; }
+    comp[i] = ci;
+    j->comp[ci].td = s[2 + 2 * i] >> 4;
+    j->comp[ci].ta = s[2 + 2 * i] & 15;
+    if (j->comp[ci].td > 3 || j->comp[ci].ta > 3) { *err = ORC_ERR_FORMAT; return NULL; }
+  }
+  int Ss = s[1 + 2 * ns], Se = s[2 + 2 * ns], Ah = s[3 + 2 * ns] >> 4, Al = s[3 + 2 * ns] & 15;
+  /* jdphuff.c start_pass_phuff_decoder: JERR_BAD_PROGRESSION cases */
+  int dcband = Ss == 0, bad = 0;
+  if (dcband) { if (Se != 0) bad = 1; }
+  else if (Ss > Se || Se > 63 || ns != 1) bad = 1;
+  if (Ah != 0 && Al != Ah - 1) bad = 1;
+  if (Al > 13) bad = 1;
+  if (bad) { *err = ORC_ERR_FORMAT; return NULL; }
+  for (int i = 0; i < ns; i++) {
+    orc_comp *cp = &j->comp[comp[i]];
+    if (dcband && Ah == 0 && !j->dc[cp->td].present) { *err = ORC_ERR_FORMAT; return NULL; }
+    if (!dcband && !j->ac[cp->ta].present) { *err = ORC_ERR_FORMAT; return NULL; }
+    for (int k = Ss; k <= Se; k++) pg->coef_bits[comp[i]][k] = Al;
+  }
+  int mcux, mcuy;
+  if (ns == 1) { /* non-interleaved: the component's own block grid */
+    orc_comp *cp = &j->comp[comp[0]];
+    mcux = (int)(((long)j->width * cp->h + 8L * j->hmax - 1) / (8L * j->hmax));
+    mcuy = (int)(((long)j->height * cp->v + 8L * j->vmax - 1) / (8L * j->vmax));
+  } else {
+    mcux = (j->width + 8 * j->hmax - 1) / (8 * j->hmax);
+    mcuy = (j->height + 8 * j->vmax - 1) / (8 * j->vmax);
+  }
+  orc_br br;
+  memset(&br, 0, sizeof(br));
+  br.p = se;
+  br.e = e;
+  int pred[4] = {0, 0, 0, 0};
+  long eobrun = 0, total = (long)mcux * mcuy, left = j->restart_interval;
+  const int p1 = 1 << Al, m1 = -1 * (1 << Al);
+  for (long m = 0; m < total; m++) {
+    if (j->restart_interval) {
+      if (left == 0) {
+        orc_restart(&br);
+        pred[0] = pred[1] = pred[2] = pred[3] = 0;
+        eobrun = 0;
+        left = j->restart_interval;
+      }
+      left--;
+    }
+    int mx = (int)(m % mcux), my = (int)(m / mcux);
+    for (int i = 0; i < ns; i++) {
+      orc_comp *cp = &j->comp[comp[i]];
+      int nbh = ns == 1 ? 1 : cp->h, nbv = ns == 1 ? 1 : cp->v;
+      for (int by = 0; by < nbv; by++)
+        for (int bx = 0; bx < nbh; bx++) {
+          int gx = ns == 1 ? mx : mx * cp->h + bx, gy = ns == 1 ? my : my * cp->v + by;
+          int16_t *blk = pg->coef[comp[i]] + ((size_t)gy * cp->bw + gx) * 64;
+          if (dcband && Ah == 0) { /* decode_mcu_DC_first */
+            int t = orc_huff_decode(&br, &j->dc[cp->td]);
+            int diff = orc_extend(orc_get(&br, t), t);
+            pred[i] += diff;
+            blk[0] = (int16_t)(pred[i] * (1 << Al));
+          } else if (dcband) { /* decode_mcu_DC_refine */
+            if (orc_get(&br, 1)) blk[0] = (int16_t)(blk[0] | p1);
+          } else if (Ah == 0) { /* decode_mcu_AC_first */
+            if (eobrun > 0) {
+              eobrun--;
+              continue;
+            }
+            for (int k = Ss; k <= Se; k++) {
+              int rs = orc_huff_decode(&br, &j->ac[cp->ta]);
+              int r = rs >> 4, t = rs & 15;
+              if (t) {
+                k += r;
+                int v = orc_extend(orc_get(&br, t), t);
+                blk[orc_natural[k]] = (int16_t)(v * (1 << Al));
+              } else if (r == 15) {
+                k += 15;
+              } else {
+                eobrun = 1L << r;
+                if (r) eobrun += orc_get(&br, r);
+                eobrun--;
+                break;
+              }
+            }
+          } else { /* decode_mcu_AC_refine */
+            int k = Ss;
+            if (eobrun == 0) {
+              for (; k <= Se; k++) {
+                int rs = orc_huff_decode(&br, &j->ac[cp->ta]);
+                int r = rs >> 4, t = rs & 15, sv = 0;
+                if (t) {
+                  sv = orc_get(&br, 1) ? p1 : m1; /* t != 1: libjpeg warns, same decode */
+                } else if (r != 15) {
+                  eobrun = 1L << r;
+                  if (r) eobrun += orc_get(&br, r);
+                  break;
+                }
+                do {
+                  int16_t *c = &blk[orc_natural[k]];
+                  if (*c != 0) orc_refine_bit(&br, c, p1, m1);
+                  else if (--r < 0) break;
+                  k++;
+                } while (k <= Se);
+                if (sv) blk[orc_natural[k]] = (int16_t)sv;
+              }
+            }
+            if (eobrun > 0) {
+              for (; k <= Se; k++) {
+                int16_t *c = &blk[orc_natural[k]];
+                if (*c != 0) orc_refine_bit(&br, c, p1, m1);
+              }
+              eobrun--;
+            }
+          }
+        }
+    }
+  }
+  if (br.hit_marker && br.marker == -1 && br.zero_fill_bits > 64) { *err = ORC_ERR_TRUNCATED; return NULL; }
+  /* next marker: the first FF xx after the data that is not stuffing or RSTn */
+  const uint8_t *q = se;
+  while (q + 1 < e) {
+    if (q[0] == 0xFF && q[1] != 0x00 && q[1] != 0xFF && !(q[1] >= 0xD0 && q[1] <= 0xD7)) return q;
+    q++;
+  }
+  *err = ORC_ERR_TRUNCATED;
+  return NULL;
+}
+
+static int orc_decode_prog(orc_jpeg *j) {
+  orc_prog pg;
+  memset(&pg, 0, sizeof(pg));
+  int rc = ORC_OK;
+  for (int c = 0; c < j->ncomp; c++) {
+    orc_comp *cp = &j->comp[c];
+    pg.coef[c] = (int16_t *)calloc((size_t)cp->bw * cp->bh * 64, sizeof(int16_t));
+    if (!pg.coef[c]) { rc = ORC_ERR_NOMEM; goto done; }
+    for (int k = 0; k < 64; k++) pg.coef_bits[c][k] = -1;
+  }
+  /* quant tables latch at a component's first scan (jdinput.c latch_quant_tables) */
+  uint16_t qlatch[4][64];
+  int latched[4] = {0, 0, 0, 0};
+  const uint8_t *p = j->sos, *e = j->end;
+  for (;;) {
+    if (p + 2 > e || p[0] != 0xFF) { rc = ORC_ERR_TRUNCATED; goto done; }
+    while (p + 1 < e && p[1] == 0xFF) p++;
+    if (p + 2 > e) { rc = ORC_ERR_TRUNCATED; goto done; }
+    int m = p[1];
+    if (m == 0xD9) break; /* EOI */
+    if (m == 0xDA) {
+      /* which components does this scan name? latch their tables first */
+      if (p + 5 > e) { rc = ORC_ERR_FORMAT; goto done; }
+      int ns = p[4];
+      for (int i = 0; i < ns && p + 5 + 2 * i < e; i++)
+        for (int c = 0; c < j->ncomp; c++)
+          if (j->comp[c].id == p[5 + 2 * i] && !latched[c]) {
+            if (!j->qt_present[j->comp[c].tq]) { rc = ORC_ERR_FORMAT; goto done; }
+            memcpy(qlatch[c], j->qt[j->comp[c].tq], sizeof(qlatch[c]));
+            latched[c] = 1;
+          }
+      int err = ORC_OK;
+      const uint8_t *nx = orc_prog_scan(j, &pg, p, &err);
+      if (!nx) { rc = err; goto done; }
+      p = nx;
+      continue;
+    }
+    if (p + 4 > e) { rc = ORC_ERR_TRUNCATED; goto done; }
+    int L = rd16(p + 2);
+    if (L < 2 || p + 2 + L > e) { rc = ORC_ERR_FORMAT; goto done; }
+    const uint8_t *s = p + 4, *se = p + 2 + L;
+    if (m == 0xC4) {
+      while (s < se) {
+        int tc = s[0] >> 4, th = s[0] & 15;
+        if (tc > 1 || th > 3 || se - s < 17) { rc = ORC_ERR_FORMAT; goto done; }
+        orc_huff *t = tc ? &j->ac[th] : &j->dc[th];
+        int count = 0;
+        for (int l = 1; l <= 16; l++) { t->bits[l] = s[l]; count += s[l]; }
+        if (count > 256 || se - s < 17 + count) { rc = ORC_ERR_FORMAT; goto done; }
+        memcpy(t->vals, s + 17, count);
+        t->present = 1;
+        orc_derive_huff(t);
+        s += 17 + count;
+      }
+    } else if (m == 0xDD) {
+      if (L != 4) { rc = ORC_ERR_FORMAT; goto done; }
+      j->restart_interval = rd16(s);
+    } else if (m == 0xDB) {
+      while (s < se) {
+        int pq = s[0] >> 4, tq = s[0] & 15, need = pq ? 129 : 65;
+        if (tq > 3 || se - s < need) { rc = ORC_ERR_FORMAT; goto done; }
+        for (int k = 0; k < 64; k++)
+          j->qt[tq][orc_natural[k]] = pq ? (uint16_t)rd16(s + 1 + 2 * k) : s[1 + k];
+        j->qt_present[tq] = 1;
+        s += need;
+      }
+    }
+    p = se;
+  }
+  for (int c = 0; c < j->ncomp; c++) {
+    if (!latched[c]) { rc = ORC_ERR_FORMAT; goto done; }
+    for (int k = 0; k < 10; k++)
+      if (pg.coef_bits[c][k] != 0) { rc = ORC_ERR_UNSUPPORTED; goto done; } /* would smooth */
+  }
+  for (int c = 0; c < j->ncomp; c++) {
+    orc_comp *cp = &j->comp[c];
+    int stride = cp->bw * 8;
+    for (int by = 0; by < cp->bh; by++)
+      for (int bx = 0; bx < cp->bw; bx++)
+        orc_idct_islow(pg.coef[c] + ((size_t)by * cp->bw + bx) * 64, qlatch[c],
+                       cp->plane + (size_t)by * 8 * stride + bx * 8, stride);
+  }
+done:
+  for (int c = 0; c < 4; c++) free(pg.coef[c]);
+  return rc;
+}
+
+/* ------------------------------------------------------------------------ */
 /* Full decode to component planes.                                          */
 /* ------------------------------------------------------------------------ */
 
@@ -498,8 +756,10 @@ static int orc_decode_planes(orc_jpeg *j) {
   }
   for (int c = 0; c < j->ncomp; c++) {
     orc_comp *cp = &j->comp[c];
-    if (!j->qt_present[cp->tq]) return ORC_ERR_FORMAT;
-    if (!j->dc[cp->td].present || !j->ac[cp->ta].present) return ORC_ERR_FORMAT;
+    if (!j->progressive) {
+      if (!j->qt_present[cp->tq]) return ORC_ERR_FORMAT;
+      if (!j->dc[cp->td].present || !j->ac[cp->ta].present) return ORC_ERR_FORMAT;
+    }
     cp->bw = mcux * cp->h;
     cp->bh = mcuy * cp->v;
     cp->dw = (int)(((long)j->width * cp->h + hmax - 1) / hmax);
@@ -507,6 +767,7 @@ static int orc_decode_planes(orc_jpeg *j) {
     cp->plane = (uint8_t *)malloc((size_t)cp->bw * 8 * cp->bh * 8);
     if (!cp->plane) return ORC_ERR_NOMEM;
   }
+  if (j->progressive) return orc_decode_prog(j);
   orc_br br;
   memset(&br, 0, sizeof(br));
   br.p = j->scan;

@@ -68,6 +68,16 @@ CASES = [
     ("q100_64x64", 64, 64, dict(quality=100), 30),
     ("noisy_256x256_q50", 256, 256, dict(quality=50), 60),
     ("flat_96x96", 96, 96, {}, 0),
+    # progressive (SOF2, libjpeg jpeg_simple_progression: spectral selection +
+    # successive approximation, EOB runs)
+    ("prog_64x80", 64, 80, dict(progressive=True), 20),
+    ("prog_375x500_q90", 375, 500, dict(quality=90, progressive=True), 20),
+    ("prog_13x17", 13, 17, dict(progressive=True), 20),
+    ("prog_1x200", 1, 200, dict(progressive=True), 20),
+    ("prog_s444_100x300", 100, 300, dict(subsampling="4:4:4", progressive=True), 20),
+    ("prog_s422_33x65", 33, 65, dict(subsampling="4:2:2", progressive=True), 20),
+    ("prog_rst_250x333_q90", 250, 333, dict(quality=90, progressive=True, restart_marker_blocks=5), 20),
+    ("prog_q100_64x64", 64, 64, dict(quality=100, progressive=True), 30),
 ]
 
 
@@ -78,6 +88,14 @@ def pil_expected(b: bytes):
     t = rs.transpose(2, 0, 1).astype(np.float32) / np.float32(255)
     tn = (t - MEAN) / STD
     return rgb, rs, t, tn
+
+
+def _cmyk(rgb) -> bytes:
+    """4-component (CMYK, Adobe) JPEG: Pillow decodes it, the build reports
+    LDT_IMG_UNSUPPORTED (ldt.h)."""
+    b = io.BytesIO()
+    Image.fromarray(rgb).convert("CMYK").save(b, format="JPEG")
+    return b.getvalue()
 
 
 def main():
@@ -122,12 +140,22 @@ def main():
                                "bytes": len(b), "label": 100, "sha256_rgb": sha(rgb),
                                "sha256_resized_u8": sha(rs), "sha256_tensor_f32": sha(t),
                                "sha256_tensor_norm_f32": sha(tn)})
+    b = io.BytesIO()
+    Image.fromarray(g).save(b, format="JPEG", progressive=True)
+    b = b.getvalue()
+    with open(os.path.join(jdir, "prog_gray_77x91.jpg"), "wb") as f:
+        f.write(b)
+    rgb, rs, t, tn = pil_expected(b)
+    manifest["images"].append({"name": "prog_gray_77x91", "file": "jpeg/prog_gray_77x91.jpg", "height": 77,
+                               "width": 91, "bytes": len(b), "label": 99, "sha256_rgb": sha(rgb),
+                               "sha256_resized_u8": sha(rs), "sha256_tensor_f32": sha(t),
+                               "sha256_tensor_norm_f32": sha(tn)})
     # bad inputs: PIL raises on each
     good = open(os.path.join(jdir, "food_384x512_q75.jpg"), "rb").read()
     bad = {
         "bad_truncated": good[: len(good) // 2],
         "bad_not_jpeg": b"\x89PNG\r\n\x1a\n" + bytes(range(200)),
-        "bad_progressive": synth.encode(synth.field(64, 80, 5), progressive=True),
+        "bad_cmyk": _cmyk(synth.field(64, 80, 5)),
         "bad_empty": b"",
     }
     for name, data in bad.items():
@@ -140,7 +168,7 @@ def main():
             raised = True
         manifest["bad"].append({"name": name, "file": f"jpeg/{name}.bin", "pil_raises": raised,
                                 "expect_status": {"bad_truncated": 3, "bad_not_jpeg": 1,
-                                                  "bad_progressive": 2, "bad_empty": 1}[name]})
+                                                  "bad_cmyk": 2, "bad_empty": 1}[name]})
     # raw HWC (config 5 path) small fixture
     raw = np.random.RandomState(5).randint(0, 256, size=(2, 300, 200, 3), dtype=np.uint8)
     exp = []

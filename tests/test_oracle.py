@@ -54,6 +54,8 @@ def test_oracle_vs_pillow_seeded(seed):
                   subsampling=str(r.choice(["4:2:0", "4:2:2", "4:4:4"])))
         if r.rand() < 0.3:
             kw["restart_marker_blocks"] = int(r.randint(1, 8))
+        if r.rand() < 0.3:
+            kw["progressive"] = True  # SOF2: jdphuff.c restatement
         b = synth.encode(synth.field(h, w, int(r.randint(1 << 30)), float(r.choice([0, 5, 30]))), **kw)
         ref = np.asarray(Image.open(io.BytesIO(b)).convert("RGB"))
         assert np.array_equal(oracle.decode_rgb(b), ref), (h, w, kw)
