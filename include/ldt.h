@@ -44,7 +44,7 @@ extern "C" {
 /* ---- per-image status codes (per_image_status[i]) ---- */
 #define LDT_IMG_OK 0
 #define LDT_IMG_NOT_JPEG 1    /* no SOI / malformed marker segments            */
-#define LDT_IMG_UNSUPPORTED 2 /* progressive, arithmetic, 12-bit, CMYK, multi-scan */
+#define LDT_IMG_UNSUPPORTED 2 /* arithmetic, lossless, 12-bit, CMYK, multi-scan sequential, or a progressive file libjpeg would block-smooth */
 #define LDT_IMG_CORRUPT 3     /* entropy data truncated or restart markers wrong */
 #define LDT_IMG_TOO_LARGE 4   /* dimension beyond LDT_MAX_DIM                  */
 #define LDT_IMG_NULL 5        /* null cell                                     */

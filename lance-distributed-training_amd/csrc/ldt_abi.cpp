@@ -53,6 +53,8 @@ struct Header {
   bool jfif = false, adobe = false;
   int adobe_transform = -1;
   int64_t scan_pos = 0; // offset of entropy-coded data within the cell
+                        // (progressive: of the first SOS marker)
+  bool progressive = false;
 };
 
 const uint8_t kZigzagToNatural[64] = {
@@ -84,7 +86,10 @@ int walk_markers(const uint8_t *cell, int64_t len, Header &H) {
     const uint8_t *e = cell + i + seglen;
     switch (m) {
     case 0xC0:
-    case 0xC1: {
+    case 0xC1:
+    case 0xC2: {
+      if (sof) return LDT_IMG_NOT_JPEG; // two SOF markers
+      H.progressive = m == 0xC2;
       if (e - s < 6) return LDT_IMG_NOT_JPEG;
       if (s[0] != 8) return LDT_IMG_UNSUPPORTED;
       H.height = be16(s + 1);
@@ -104,7 +109,7 @@ int walk_markers(const uint8_t *cell, int64_t len, Header &H) {
       sof = true;
       break;
     }
-    case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA:
+    case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA:
     case 0xCB: case 0xCD: case 0xCE: case 0xCF:
       return LDT_IMG_UNSUPPORTED;
     case 0xC4: {
@@ -153,6 +158,10 @@ int walk_markers(const uint8_t *cell, int64_t len, Header &H) {
       break;
     case 0xDA: {
       if (!sof) return LDT_IMG_NOT_JPEG;
+      if (H.progressive) { // every scan is walked by plan_progressive
+        H.scan_pos = i - 2;
+        return LDT_IMG_OK;
+      }
       const int ns = s[0];
       if (ns < 1 || ns > 4 || e - s < 4 + 2 * ns) return LDT_IMG_NOT_JPEG;
       if (ns != H.ncomp) return LDT_IMG_UNSUPPORTED; // multi-scan sequential
@@ -251,6 +260,175 @@ std::string huff_key(const RawHuff &r, bool dc) {
   k.append(reinterpret_cast<const char *>(r.counts), 16);
   k.append(reinterpret_cast<const char *>(r.syms), r.nsym);
   return k;
+}
+
+// ---- progressive (SOF2) planning ----------------------------------------
+// Table for k_prog: canonical codes as jdhuff.c jpeg_make_d_derived_tbl
+// (same validity checks as build_huff), plus the 8-bit lookahead.
+bool build_prog_tab(const RawHuff &r, bool is_dc, ProgTab &t) {
+  memset(&t, 0, sizeof(t));
+  int code = 0, k = 0;
+  int lens[256], codes[256];
+  for (int l = 1; l <= 16; ++l) {
+    const int cnt = r.counts[l - 1];
+    if (cnt) {
+      t.valoff[l] = k - code;
+      for (int j = 0; j < cnt; ++j, ++k, ++code) {
+        lens[k] = l;
+        codes[k] = code;
+      }
+      t.maxcode[l] = code - 1;
+    } else {
+      t.maxcode[l] = -1;
+    }
+    if (cnt && code >= (1 << l)) return false; // all-ones code: JERR_BAD_HUFF_TABLE
+    code <<= 1;
+  }
+  t.maxcode[17] = 0x7FFFFFFF;
+  for (int j = 0; j < r.nsym; ++j) {
+    t.vals[j] = r.syms[j];
+    if (is_dc && r.syms[j] > 15) return false;
+    if (lens[j] <= 8) {
+      const int base = codes[j] << (8 - lens[j]);
+      for (int x = 0; x < (1 << (8 - lens[j])); ++x)
+        t.look[base + x] = (uint16_t)((lens[j] << 8) | r.syms[j]);
+    }
+  }
+  return true;
+}
+
+struct ProgPlan {
+  std::vector<ProgScan> scans;                // tab[]: indices into tabs
+  std::vector<std::pair<RawHuff, bool>> tabs; // (table, is_dc)
+  uint16_t q[4][64];                          // latched quant tables, natural order
+};
+
+// Walks every scan of a progressive image from its first SOS (H.scan_pos):
+// jdmarker.c between scans (DHT / DQT / DRI), jdphuff.c
+// start_pass_phuff_decoder's progression checks, jdinput.c's quant table
+// latch at a component's first scan, and the byte range of each scan's
+// entropy-coded data (up to the first marker that is not RSTn). Files whose
+// coefficients 0..9 are not fully refined after the last scan would take
+// libjpeg's block-smoothing path (jdcoefct.c smoothing_ok): unsupported.
+// Returns an LDT_IMG_* code.
+int plan_progressive(const uint8_t *cell, int64_t len, const Header &H0, ProgPlan &P) {
+  Header H = H0;
+  int coef_bits[4][10];
+  bool latched[4] = {false, false, false, false};
+  for (int c = 0; c < 4; ++c)
+    for (int k = 0; k < 10; ++k) coef_bits[c][k] = -1;
+  int64_t i = H0.scan_pos;
+  while (true) {
+    if (i + 1 >= len || cell[i] != 0xFF) return LDT_IMG_CORRUPT; // data ended before EOI
+    while (i + 1 < len && cell[i + 1] == 0xFF) ++i;
+    if (i + 1 >= len) return LDT_IMG_CORRUPT;
+    const int m = cell[i + 1];
+    i += 2;
+    if (m == 0xD9) break;
+    if (m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+    if (i + 2 > len) return LDT_IMG_CORRUPT;
+    const int seglen = be16(cell + i);
+    if (seglen < 2 || i + seglen > len) return LDT_IMG_CORRUPT;
+    const uint8_t *s = cell + i + 2;
+    const uint8_t *e = cell + i + seglen;
+    if (m == 0xC4) {
+      while (s < e) {
+        const int tc = s[0] >> 4, th = s[0] & 15;
+        if (tc > 1 || th > 3 || e - s < 17) return LDT_IMG_NOT_JPEG;
+        RawHuff &t = tc ? H.ac[th] : H.dc[th];
+        int n = 0;
+        for (int l = 0; l < 16; ++l) {
+          t.counts[l] = s[1 + l];
+          n += s[1 + l];
+        }
+        if (n > 256 || e - s < 17 + n) return LDT_IMG_NOT_JPEG;
+        memcpy(t.syms, s + 17, n);
+        t.nsym = n;
+        t.present = true;
+        s += 17 + n;
+      }
+    } else if (m == 0xDB) {
+      while (s < e) {
+        const int pq = s[0] >> 4, tq = s[0] & 15;
+        if (tq > 3 || pq > 1) return LDT_IMG_NOT_JPEG;
+        const int need = pq ? 129 : 65;
+        if (e - s < need) return LDT_IMG_NOT_JPEG;
+        for (int k = 0; k < 64; ++k)
+          H.q[tq][kZigzagToNatural[k]] = pq ? (uint16_t)be16(s + 1 + 2 * k) : s[1 + k];
+        H.qpresent[tq] = true;
+        s += need;
+      }
+    } else if (m == 0xDD) {
+      if (seglen != 4) return LDT_IMG_NOT_JPEG;
+      H.restart = be16(s);
+    } else if (m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+      return LDT_IMG_NOT_JPEG; // a second frame header
+    } else if (m == 0xDA) {
+      const int ns = s[0];
+      if (ns < 1 || ns > 4 || e - s < 4 + 2 * ns) return LDT_IMG_NOT_JPEG;
+      ProgScan sc;
+      memset(&sc, 0, sizeof(sc));
+      sc.ns = ns;
+      sc.ss = s[1 + 2 * ns];
+      sc.se = s[2 + 2 * ns];
+      sc.ah = s[3 + 2 * ns] >> 4;
+      sc.al = s[3 + 2 * ns] & 15;
+      sc.restart = H.restart;
+      const bool dcband = sc.ss == 0;
+      bool bad = dcband ? sc.se != 0 : (sc.ss > sc.se || sc.se > 63 || ns != 1);
+      if (sc.ah != 0 && sc.al != sc.ah - 1) bad = true;
+      if (sc.al > 13) bad = true;
+      if (bad) return LDT_IMG_CORRUPT; // JERR_BAD_PROGRESSION
+      for (int k = 0; k < 4; ++k) sc.tab[k] = -1;
+      for (int k = 0; k < ns; ++k) {
+        int idx = -1;
+        for (int c = 0; c < H.ncomp; ++c)
+          if (H.cid[c] == s[1 + 2 * k]) idx = c;
+        if (idx < 0) return LDT_IMG_NOT_JPEG;
+        sc.comp[k] = idx;
+        const int td = s[2 + 2 * k] >> 4, ta = s[2 + 2 * k] & 15;
+        if (td > 3 || ta > 3) return LDT_IMG_NOT_JPEG;
+        if (!latched[idx]) {
+          if (!H.qpresent[H.tq[idx]]) return LDT_IMG_NOT_JPEG;
+          memcpy(P.q[idx], H.q[H.tq[idx]], sizeof(P.q[idx]));
+          latched[idx] = true;
+        }
+        const RawHuff *t = nullptr;
+        bool is_dc = false;
+        if (dcband && sc.ah == 0) {
+          t = &H.dc[td];
+          is_dc = true;
+        } else if (!dcband && k == 0) {
+          t = &H.ac[ta];
+        }
+        if (t) {
+          if (!t->present) return LDT_IMG_NOT_JPEG;
+          sc.tab[k] = (int32_t)P.tabs.size();
+          P.tabs.emplace_back(*t, is_dc);
+        }
+        for (int q = sc.ss; q <= sc.se && q < 10; ++q) coef_bits[idx][q] = sc.al;
+      }
+      const int64_t start = i + seglen;
+      int64_t j = start;
+      while (j + 1 < len && !(cell[j] == 0xFF && cell[j + 1] != 0x00 && cell[j + 1] != 0xFF &&
+                              !(cell[j + 1] >= 0xD0 && cell[j + 1] <= 0xD7)))
+        ++j;
+      if (j + 1 >= len) return LDT_IMG_CORRUPT; // truncated inside the scan
+      sc.data_off = start;
+      sc.data_len = j - start;
+      P.scans.push_back(sc);
+      if ((int)P.scans.size() > kMaxProgScans) return LDT_IMG_UNSUPPORTED;
+      i = j;
+      continue;
+    }
+    i += seglen;
+  }
+  for (int c = 0; c < H.ncomp; ++c) {
+    if (!latched[c]) return LDT_IMG_NOT_JPEG;
+    for (int k = 0; k < 10; ++k)
+      if (coef_bits[c][k] != 0) return LDT_IMG_UNSUPPORTED; // would be block-smoothed
+  }
+  return LDT_IMG_OK;
 }
 
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
@@ -560,6 +738,10 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   std::vector<int32_t> chunk_img;
   int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3, max_tabs = 1, n_fast420 = 0;
   int max_sub_bits = 64; // largest per-image S: sizes the decoders' LDS window
+  std::vector<ProgScan> pscans;  // progressive images' scans (k_prog)
+  std::vector<ProgTab> ptabs;
+  std::unordered_map<std::string, int> ptab_map;
+  std::vector<int32_t> prog_img;
   bool any_bad = false;
   for (int64_t i = 0; i < n; ++i) {
     ImgPlan &ip = P[(size_t)i];
@@ -582,7 +764,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     int hmax = 1, vmax = 1;
     if (ip.status == LDT_IMG_OK) {
       for (int k = 0; k < H.ncomp; ++k) {
-        if (!H.qpresent[H.tq[k]] || !H.dc[H.td[k]].present || !H.ac[H.ta[k]].present) {
+        if (!H.progressive &&
+            (!H.qpresent[H.tq[k]] || !H.dc[H.td[k]].present || !H.ac[H.ta[k]].present)) {
           ip.status = LDT_IMG_NOT_JPEG;
           break;
         }
@@ -644,6 +827,17 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       }
       d.bpm = b;
     }
+    ProgPlan PP;
+    if (H.progressive) {
+      ip.status = plan_progressive(cells_host + ip.cell_off, ip.cell_len, H, PP);
+      if (ip.status != LDT_IMG_OK) {
+        st[(size_t)i] = ip.status;
+        any_bad = true;
+        d.width = d.height = 1;
+        d.nseg = 0;
+        continue;
+      }
+    }
     int64_t pl = plane_total;
     for (int k = 0; k < H.ncomp; ++k) {
       const int bw = d.mcux * d.ch[k], bh = d.mcuy * d.cv[k];
@@ -656,16 +850,17 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
         d.cdw[k] = H.width;
         d.cdh[k] = H.height;
       }
-      // quant table
-      std::string qk(reinterpret_cast<const char *>(H.q[H.tq[k]]), 128);
+      // quant table (progressive: latched at the component's first scan)
+      const uint16_t *qsrc = H.progressive ? PP.q[k] : H.q[H.tq[k]];
+      std::string qk(reinterpret_cast<const char *>(qsrc), 128);
       auto qi = qmap.find(qk);
       if (qi == qmap.end()) {
         qi = qmap.emplace(qk, (int)qtabs.size()).first;
-        qtabs.emplace_back(H.q[H.tq[k]], H.q[H.tq[k]] + 64);
+        qtabs.emplace_back(qsrc, qsrc + 64);
       }
       d.qt[k] = qi->second;
       // Huffman tables (deduped across the context's lifetime)
-      for (int pass = 0; pass < 2; ++pass) {
+      for (int pass = 0; pass < 2 && !H.progressive; ++pass) {
         const RawHuff &rh = pass == 0 ? H.dc[H.td[k]] : H.ac[H.ta[k]];
         std::string key = huff_key(rh, pass == 0);
         auto it = c->hmap.find(key);
@@ -702,7 +897,49 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       d.width = d.height = 1;
       continue;
     }
-    {
+    if (H.progressive) {
+      // k_prog decodes it: no baseline segments, destuff chunks or decoder
+      // workgroups; its scans join the batch's scan table
+      plane_total = pl;
+      d.restart = 0;
+      d.nseg = 0;
+      d.wg_first = n_wg;
+      d.ds_first = n_chunks;
+      d.dst_off = dst_total;
+      d.prog_first = (int32_t)pscans.size();
+      d.prog_count = (int32_t)PP.scans.size();
+      for (ProgScan sc : PP.scans) {
+        sc.data_off += ip.cell_off;
+        for (int k = 0; k < 4; ++k) {
+          if (sc.tab[k] < 0) continue;
+          const auto &rt = PP.tabs[(size_t)sc.tab[k]];
+          std::string key = huff_key(rt.first, rt.second);
+          auto it = ptab_map.find(key);
+          if (it == ptab_map.end()) {
+            ProgTab t;
+            if (!build_prog_tab(rt.first, rt.second, t)) {
+              ip.status = LDT_IMG_NOT_JPEG;
+              break;
+            }
+            it = ptab_map.emplace(std::move(key), (int)ptabs.size()).first;
+            ptabs.push_back(t);
+          }
+          sc.tab[k] = it->second;
+        }
+        pscans.push_back(sc);
+      }
+      if (ip.status != LDT_IMG_OK) {
+        pscans.resize((size_t)d.prog_first);
+        st[(size_t)i] = ip.status;
+        any_bad = true;
+        d.nseg = 0;
+        d.prog_count = 0;
+        d.width = d.height = 1;
+        continue;
+      }
+      prog_img.push_back((int32_t)i);
+    }
+    if (!H.progressive) {
       // distinct tables over the image's (component, DC/AC) contexts
       int ids[6], nd = 0;
       for (int x = 0; x < 6; ++x) {
@@ -714,9 +951,10 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       }
       if (nd > max_tabs) max_tabs = nd;
     }
+    const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
+    if (!H.progressive) {
     plane_total = pl;
     d.restart = H.restart;
-    const int64_t nmcu = (int64_t)d.mcux * d.mcuy;
     d.nseg = H.restart ? (int32_t)((nmcu + H.restart - 1) / H.restart) : 1;
     for (int sidx = 0; sidx < d.nseg; ++sidx) {
       Segment sg;
@@ -761,6 +999,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     n_chunks += d.ds_count;
     d.dst_off = dst_total;
     dst_total += align_up(d.src_len + 16 + (int64_t)kSegPad * d.nseg, 16);
+    } // !progressive
     d.coef_off = coef_blocks;
     const int64_t nblk = nmcu * d.bpm;
     coef_blocks += nblk;
@@ -801,6 +1040,12 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   off = align_up(off + 4 * (int64_t)n_chunks, 64);
   const int64_t off_redo = off;
   off = align_up(off + 64, 64);
+  const int64_t off_pscan = off;
+  off = align_up(off + (int64_t)sizeof(ProgScan) * (int64_t)pscans.size(), 64);
+  const int64_t off_ptab = off;
+  off = align_up(off + (int64_t)sizeof(ProgTab) * (int64_t)ptabs.size(), 64);
+  const int64_t off_pimg = off;
+  off = align_up(off + 4 * (int64_t)prog_img.size(), 64);
   const int64_t plan_bytes = off;
   ph.has_labels = labels ? 1 : 0;
   ph.max_ks_h = max_ks_h;
@@ -825,6 +1070,9 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if (n_wg) memcpy(hp + off_wg, wg_img.data(), 4 * (size_t)n_wg);
   if (n_chunks) memcpy(hp + off_chunk, chunk_img.data(), 4 * (size_t)n_chunks);
   memset(hp + off_redo, 0, 64);
+  if (!pscans.empty()) memcpy(hp + off_pscan, pscans.data(), sizeof(ProgScan) * pscans.size());
+  if (!ptabs.empty()) memcpy(hp + off_ptab, ptabs.data(), sizeof(ProgTab) * ptabs.size());
+  if (!prog_img.empty()) memcpy(hp + off_pimg, prog_img.data(), 4 * prog_img.size());
 
   // ---- device workspace ----
   if ((rc = ensure_dev(c, c->d_plan, (size_t)plan_bytes, s))) return rc;
@@ -883,6 +1131,10 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
   p.max_tabs = max_tabs;
   p.n_fast420 = n_fast420;
+  p.n_prog = (int)prog_img.size();
+  p.prog_img = reinterpret_cast<const int32_t *>(dp + off_pimg);
+  p.pscans = reinterpret_cast<const ProgScan *>(dp + off_pscan);
+  p.ptabs = reinterpret_cast<const ProgTab *>(dp + off_ptab);
   c->last_off_redo = off_redo;
   DevWork w;
   w.data = dev_cells;
@@ -900,6 +1152,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   c->coef_dirty = true;
   if (parallel) HIPCHK(c, launch_huff_parallel(p, w, s));
   else HIPCHK(c, launch_huff_serial(p, w, s));
+  HIPCHK(c, launch_prog(p, w, s));
   HIPCHK(c, launch_dc_scan(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
   if (!(c->debug_skip & 2)) HIPCHK(c, launch_idct(p, w, s));

@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
                                                     int16_t *__restrict__ dcv,
                                                     int32_t *__restrict__ status) {
   const int img = blockIdx.x;
-  if (status[img] != 0) return;
+  if (status[img] != 0 || descs[img].nseg == 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
   const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, tid, 64);
@@ -366,7 +366,7 @@ __global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ des
   __shared__ int s_f[256];
   __shared__ int s_v[3][256];
   const int img = blockIdx.x;
-  if (status[img] != 0) return;
+  if (status[img] != 0 || descs[img].nseg == 0) return; // progressive: dcv holds final DC
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
   const int bpm = d.bpm;
@@ -863,7 +863,7 @@ __global__ void __launch_bounds__(64) k_huff_fix_serial(const ImgDesc *__restric
                                                         const int32_t *__restrict__ status,
                                                         const int32_t *__restrict__ redo) {
   const int img = blockIdx.x;
-  if (redo[0] == 0 || status[img] != 0) return;
+  if (redo[0] == 0 || status[img] != 0 || descs[img].nseg == 0) return;
   const ImgDesc &d = descs[img];
   const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, threadIdx.x, 64);
   __syncthreads();
@@ -885,7 +885,7 @@ __global__ void __launch_bounds__(256) k_huff_scan(const ImgDesc *__restrict__ d
                                                    const int32_t *__restrict__ status) {
   __shared__ int sh_scan[8];
   const int img = blockIdx.x;
-  if (status[img] != 0) return;
+  if (status[img] != 0 || descs[img].nseg == 0) return;
   const ImgDesc &d = descs[img];
   const Segment &last = segs[d.seg_base + d.nseg - 1];
   const int total = last.sub_first + last.sub_count;

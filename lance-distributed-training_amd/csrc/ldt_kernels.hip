@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
   __shared__ int sh_endc;
   const int img = blockIdx.x, tid = threadIdx.x;
   const ImgDesc &d = descs[img];
-  if (status[img] != 0) return;
+  if (status[img] != 0 || d.nseg == 0) return; // nseg 0: progressive (k_prog)
   // chunks up to and including the first one holding the end-of-scan marker
   if (tid == 0) sh_endc = d.ds_count;
   __syncthreads();

@@ -37,6 +37,11 @@ struct DevPlan {
   int32_t *redo;         // set when a workgroup-boundary walk did not converge
   int max_tabs;          // max distinct Huffman tables of one image (LDS slots)
   int n_fast420;         // images on k_resize4's fast staging path (resize_fast420)
+  // progressive images (k_prog, one workgroup each)
+  int n_prog;
+  const int32_t *prog_img; // -> image index
+  const ProgScan *pscans;
+  const ProgTab *ptabs;
   // destuff chunks (4 KB of entropy-coded bytes each)
   int n_chunks;
   const int32_t *chunk_img; // chunk -> image
@@ -60,6 +65,8 @@ hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s)
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s);
+// Progressive (SOF2) images: serial per-scan decode into coef/dcv (ldt_prog.hip).
+hipError_t launch_prog(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
                               hipStream_t s);
 // Banded resize (ldt_resize.hip). Return false when the geometry does not fit

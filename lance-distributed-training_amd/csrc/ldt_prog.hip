@@ -1,0 +1,368 @@
+// ldt_prog.hip — entropy decode of progressive JPEG (SOF2) images.
+//
+// jdphuff.c restated (decode_mcu_DC_first / DC_refine / AC_first / AC_refine,
+// EOB runs, restart intervals) with jdcoefct.c's full-image coefficient
+// buffer: every scan updates the image's blocks in the same coefficient
+// buffer the baseline decoder fills (zigzag slots 1..63 in `coef`, the final
+// DC value in `dcv`), so k_idct and the resize kernels then run unchanged.
+//
+// One 64-lane workgroup per progressive image. A scan's Huffman decode is a
+// serial bit stream, so lane 0 decodes while the other lanes stage its
+// inputs: the scan's bytes in an LDS window, and the coefficients of the next
+// 64 blocks (one block per lane, coalesced 16-byte loads) which lane 0 then
+// reads and refines in LDS before the wave writes them back. Scans run in
+// file order (a refinement scan depends on the earlier scans of its band).
+//
+// Reference semantics: libjpeg-turbo jdphuff.c (Pillow 12.2.0's decoder),
+// jdhuff.c jpeg_fill_bit_buffer (byte stuffing, zero bits at a marker),
+// process_restart. The host (ldt_abi.cpp plan_progressive) has already
+// checked the progression parameters, found each scan's byte range and
+// rejected files that libjpeg would block-smooth.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ldt_device.hpp"
+#include "ldt_kernels.hpp"
+
+namespace ldt {
+
+namespace {
+
+constexpr int kWin = 16384; // scan bytes staged in LDS
+constexpr int kChunk = 64;  // blocks staged per round (one per lane)
+
+struct ProgLds {
+  uint8_t win[kWin];
+  __attribute__((aligned(16))) int16_t blk[kChunk][64]; // zigzag slots; [0] unused
+  int16_t dc[kChunk];
+  int64_t bidx[kChunk]; // coefficient-buffer block index of each staged slot
+  ProgTab tabs[4];
+  int64_t win_base, win_lim; // data offsets of win[0] and one past its last valid byte
+  int64_t pos;               // lane 0's reader position (for window refills)
+};
+
+// Lane 0's bit reader: jdhuff.c semantics (MSB first, FF00 -> FF, FF fill
+// bytes skipped, zero bits once a marker is reached).
+struct PReader {
+  const uint8_t *data;
+  int64_t pos, lim; // lim: one past the marker that ends the scan
+  uint64_t buf;
+  int bits;
+  int marker; // 0: none yet; else the marker code reached
+};
+
+__device__ __forceinline__ int pbyte(const ProgLds &L, const uint8_t *data, int64_t p) {
+  const int64_t o = p - L.win_base;
+  return (o >= 0 && p < L.win_lim) ? L.win[o] : data[p];
+}
+
+__device__ __forceinline__ void pfill(PReader &r, const ProgLds &L) {
+  while (r.bits <= 56) {
+    int c = 0;
+    if (r.marker == 0 && r.pos < r.lim) {
+      c = pbyte(L, r.data, r.pos++);
+      if (c == 0xFF) {
+        int c2;
+        do {
+          c2 = r.pos < r.lim ? pbyte(L, r.data, r.pos++) : 0x100;
+        } while (c2 == 0xFF);
+        if (c2 == 0) {
+          c = 0xFF;
+        } else {
+          r.marker = c2; // RSTn or the marker that ends the scan
+          c = 0;
+        }
+      }
+    }
+    r.buf |= (uint64_t)c << (56 - r.bits);
+    r.bits += 8;
+  }
+}
+
+__device__ __forceinline__ int pget(PReader &r, const ProgLds &L, int n) {
+  if (n == 0) return 0;
+  if (r.bits < n) pfill(r, L);
+  const int v = (int)(r.buf >> (64 - n));
+  r.buf <<= n;
+  r.bits -= n;
+  return v;
+}
+
+// jdhuff.c jpeg_huff_decode: 8-bit lookahead, then the canonical search.
+__device__ __forceinline__ int phuff(PReader &r, const ProgLds &L, const ProgTab &t) {
+  if (r.bits < 16) pfill(r, L);
+  const uint32_t e = t.look[r.buf >> 56];
+  if (e) {
+    const int l = (int)(e >> 8);
+    r.buf <<= l;
+    r.bits -= l;
+    return (int)(e & 255);
+  }
+  const int w = (int)(r.buf >> 48);
+  for (int l = 9; l <= 16; ++l) {
+    const int code = w >> (16 - l);
+    if (code <= t.maxcode[l]) {
+      r.buf <<= l;
+      r.bits -= l;
+      return t.vals[(t.valoff[l] + code) & 0xFF];
+    }
+  }
+  r.buf <<= 16; // corrupt data: libjpeg warns and returns symbol 0
+  r.bits -= 16;
+  return 0;
+}
+
+__device__ __forceinline__ int pextend(int v, int s) {
+  return s == 0 ? 0 : (v < (1 << (s - 1)) ? v - (1 << s) + 1 : v);
+}
+
+// jdphuff.c process_restart: drop the buffered bits and consume RSTn.
+__device__ __forceinline__ void prestart(PReader &r, const ProgLds &L) {
+  r.buf = 0;
+  r.bits = 0;
+  if (r.marker >= 0xD0 && r.marker <= 0xD7) {
+    r.marker = 0;
+    return;
+  }
+  if (r.marker != 0) return; // another marker: zero bits for the rest of the scan
+  while (r.pos + 1 < r.lim) {
+    const int a = pbyte(L, r.data, r.pos), b = pbyte(L, r.data, r.pos + 1);
+    if (a == 0xFF && b >= 0xD0 && b <= 0xD7) {
+      r.pos += 2;
+      return;
+    }
+    if (a == 0xFF && b != 0x00 && b != 0xFF) return;
+    ++r.pos;
+  }
+}
+
+// AC refinement correction bit on an already-nonzero coefficient.
+__device__ __forceinline__ void prefine(PReader &r, const ProgLds &L, int16_t &c, int p1, int m1) {
+  if (pget(r, L, 1) && (c & p1) == 0) c = (int16_t)(c >= 0 ? c + p1 : c + m1);
+}
+
+// Stage scan bytes [base, min(base + kWin, lim)) into the window (all lanes).
+__device__ void load_window(ProgLds &L, const uint8_t *data, int64_t base, int64_t lim) {
+  const int lane = threadIdx.x;
+  const int64_t n = min((int64_t)kWin, lim - base);
+  for (int64_t o = lane; o < n; o += 64) L.win[o] = data[base + o];
+  if (lane == 0) {
+    L.win_base = base;
+    L.win_lim = base + n;
+  }
+}
+
+} // namespace
+
+__global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
+                                             const int32_t *__restrict__ prog_img,
+                                             const ProgScan *__restrict__ scans,
+                                             const ProgTab *__restrict__ ptabs,
+                                             const uint8_t *__restrict__ data,
+                                             int16_t *__restrict__ coef,
+                                             int16_t *__restrict__ dcv,
+                                             const int32_t *__restrict__ status) {
+  __shared__ ProgLds L;
+  const int img = prog_img[blockIdx.x];
+  if (status[img] != 0) return;
+  const ImgDesc &d = descs[img];
+  const int lane = threadIdx.x;
+  const int64_t nblk = (int64_t)d.mcux * d.mcuy * d.bpm;
+  // DC values start at zero: blocks no DC scan covers (the padding blocks of
+  // non-interleaved DC scans) must not keep an earlier batch's value
+  for (int64_t b = lane; b < nblk; b += 64) dcv[d.coef_off + b] = 0;
+  int b0[3] = {0, 0, 0}, hmax = 1, vmax = 1;
+  for (int c = 0; c < d.ncomp; ++c) {
+    hmax = max(hmax, d.ch[c]);
+    vmax = max(vmax, d.cv[c]);
+    for (int b = d.bpm - 1; b >= 0; --b)
+      if (d.bcomp[b] == c) b0[c] = b;
+  }
+  PReader R;
+  R.data = data;
+  int pred[4] = {0, 0, 0, 0};
+  for (int si = 0; si < d.prog_count; ++si) {
+    const ProgScan &sc = scans[d.prog_first + si];
+    const int ns = sc.ns, Ss = sc.ss, Se = sc.se, Ah = sc.ah, Al = sc.al;
+    const bool dcband = Ss == 0;
+    __syncthreads();
+    for (int k = 0; k < 4; ++k) {
+      if (sc.tab[k] < 0) continue;
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(ptabs + sc.tab[k]);
+      uint32_t *dst = reinterpret_cast<uint32_t *>(&L.tabs[k]);
+      for (int o = lane; o < (int)(sizeof(ProgTab) / 4); o += 64) dst[o] = src[o];
+    }
+    const int64_t lim = sc.data_off + sc.data_len + 2; // through the ending marker
+    load_window(L, data, sc.data_off, lim);
+    __syncthreads();
+    // units: MCUs of the interleaved grid, or the component's own blocks
+    int ux, uy, bpu = 0;
+    if (ns == 1) {
+      const int c = sc.comp[0];
+      ux = (int)(((int64_t)d.width * d.ch[c] + 8 * hmax - 1) / (8 * hmax));
+      uy = (int)(((int64_t)d.height * d.cv[c] + 8 * vmax - 1) / (8 * vmax));
+      if (d.ncomp == 1) {
+        ux = d.mcux;
+        uy = d.mcuy;
+      }
+      bpu = 1;
+    } else {
+      ux = d.mcux;
+      uy = d.mcuy;
+      for (int i = 0; i < ns; ++i) bpu += d.ch[sc.comp[i]] * d.cv[sc.comp[i]];
+    }
+    const int64_t units = (int64_t)ux * uy;
+    const int upc = kChunk / bpu;
+    R.pos = sc.data_off;
+    R.lim = lim;
+    R.buf = 0;
+    R.bits = 0;
+    R.marker = 0;
+    pred[0] = pred[1] = pred[2] = pred[3] = 0;
+    int64_t eobrun = 0;
+    int togo = sc.restart;
+    const int p1 = 1 << Al, m1 = -(1 << Al);
+    for (int64_t u0 = 0; u0 < units; u0 += upc) {
+      const int nu = (int)min((int64_t)upc, units - u0);
+      const int nbk = nu * bpu;
+      // stage the chunk's blocks: lane j -> block j of the chunk, scan order
+      if (lane < nbk) {
+        const int64_t u = u0 + lane / bpu;
+        int64_t blk;
+        if (ns == 1) {
+          const int c = sc.comp[0];
+          const int bx = (int)(u % ux), by = (int)(u / ux);
+          const int64_t m = (int64_t)(by / d.cv[c]) * d.mcux + bx / d.ch[c];
+          blk = m * d.bpm + b0[c] + (by % d.cv[c]) * d.ch[c] + (bx % d.ch[c]);
+        } else {
+          int j = lane % bpu, b = 0;
+          for (int i = 0; i < ns; ++i) {
+            const int c = sc.comp[i], nb = d.ch[c] * d.cv[c];
+            if (j >= 0 && j < nb) b = b0[c] + j;
+            j -= nb;
+          }
+          blk = u * d.bpm + b;
+        }
+        const int64_t gb = d.coef_off + blk;
+        L.bidx[lane] = gb;
+        if (dcband) {
+          L.dc[lane] = dcv[gb];
+        } else {
+          const int4 *src = reinterpret_cast<const int4 *>(coef + gb * 64);
+          int4 *dst = reinterpret_cast<int4 *>(L.blk[lane]);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) dst[q] = src[q];
+        }
+      }
+      __syncthreads();
+      if (lane == 0) {
+        int slot = 0;
+        for (int ui = 0; ui < nu; ++ui) {
+          if (sc.restart) {
+            if (togo == 0) {
+              prestart(R, L);
+              pred[0] = pred[1] = pred[2] = pred[3] = 0;
+              eobrun = 0;
+              togo = sc.restart;
+            }
+            --togo;
+          }
+          for (int i = 0; i < ns; ++i) {
+            const int nb = ns == 1 ? 1 : d.ch[sc.comp[i]] * d.cv[sc.comp[i]];
+            for (int q = 0; q < nb; ++q, ++slot) {
+              if (dcband && Ah == 0) { // decode_mcu_DC_first
+                const int t = phuff(R, L, L.tabs[i]);
+                pred[i] += pextend(pget(R, L, t), t);
+                L.dc[slot] = (int16_t)(pred[i] * (1 << Al));
+              } else if (dcband) { // decode_mcu_DC_refine
+                if (pget(R, L, 1)) L.dc[slot] = (int16_t)(L.dc[slot] | p1);
+              } else if (Ah == 0) { // decode_mcu_AC_first
+                if (eobrun > 0) {
+                  --eobrun;
+                  continue;
+                }
+                int16_t *blk = L.blk[slot];
+                for (int k = Ss; k <= Se; ++k) {
+                  const int rs = phuff(R, L, L.tabs[0]);
+                  const int r = rs >> 4, t = rs & 15;
+                  if (t) {
+                    k += r;
+                    blk[min(k, 63)] = (int16_t)(pextend(pget(R, L, t), t) * (1 << Al));
+                  } else if (r == 15) {
+                    k += 15;
+                  } else {
+                    eobrun = (int64_t)1 << r;
+                    if (r) eobrun += pget(R, L, r);
+                    --eobrun;
+                    break;
+                  }
+                }
+              } else { // decode_mcu_AC_refine
+                int16_t *blk = L.blk[slot];
+                int k = Ss;
+                if (eobrun == 0) {
+                  for (; k <= Se; ++k) {
+                    const int rs = phuff(R, L, L.tabs[0]);
+                    int r = rs >> 4;
+                    const int t = rs & 15;
+                    int sv = 0;
+                    if (t) {
+                      sv = pget(R, L, 1) ? p1 : m1;
+                    } else if (r != 15) {
+                      eobrun = (int64_t)1 << r;
+                      if (r) eobrun += pget(R, L, r);
+                      break;
+                    }
+                    do {
+                      int16_t &c = blk[min(k, 63)];
+                      if (c != 0) prefine(R, L, c, p1, m1);
+                      else if (--r < 0) break;
+                      ++k;
+                    } while (k <= Se);
+                    if (sv) blk[min(k, 63)] = (int16_t)sv;
+                  }
+                }
+                if (eobrun > 0) {
+                  for (; k <= Se; ++k) {
+                    int16_t &c = blk[k];
+                    if (c != 0) prefine(R, L, c, p1, m1);
+                  }
+                  --eobrun;
+                }
+              }
+            }
+          }
+        }
+        L.pos = R.pos;
+      }
+      __syncthreads();
+      if (lane < nbk) {
+        const int64_t gb = L.bidx[lane];
+        if (dcband) {
+          dcv[gb] = L.dc[lane];
+        } else {
+          int4 *dst = reinterpret_cast<int4 *>(coef + gb * 64);
+          const int4 *src = reinterpret_cast<const int4 *>(L.blk[lane]);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) dst[q] = src[q];
+        }
+      }
+      // keep at least half a window of bytes ahead of the reader
+      const int64_t pos = L.pos;
+      if (pos - L.win_base > kWin / 2 && L.win_lim < lim) {
+        __syncthreads();
+        load_window(L, data, pos, lim);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+hipError_t launch_prog(const DevPlan &p, const DevWork &w, hipStream_t s) {
+  if (p.n_prog == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prog, dim3(p.n_prog), dim3(64), 0, s, p.descs, p.prog_img, p.pscans, p.ptabs,
+                     w.data, w.coef, w.dcv, w.status);
+  return hipGetLastError();
+}
+
+} // namespace ldt

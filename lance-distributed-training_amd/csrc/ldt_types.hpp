@@ -42,6 +42,9 @@ struct ImgDesc {
   // destuff: this image's 4 KB chunks are [ds_first, ds_first + ds_count)
   int32_t ds_first, ds_count;
   int32_t sub_bits;  // parallel Huffman subsequence length S of this image (bits)
+  // progressive (SOF2) images: scans [prog_first, prog_first + prog_count) of
+  // the plan's scan table, decoded by k_prog; nseg == 0 (no baseline segments)
+  int32_t prog_first, prog_count;
 };
 
 // k_resize4's fast staging path: 4:2:0 YCbCr with both chroma planes
@@ -121,6 +124,29 @@ struct HuffTab {
   int32_t valoff[18];
   uint8_t vals[256];
 };
+
+// One scan of a progressive image (jdphuff.c start_pass_phuff_decoder
+// parameters), in file order.
+struct ProgScan {
+  int32_t ss, se, ah, al; // spectral band [ss, se], successive approximation
+  int32_t ns;             // components in the scan (> 1 only for DC scans)
+  int32_t restart;        // restart interval (MCUs) in force for the scan
+  int32_t comp[4];        // frame component index of each scan component
+  int32_t tab[4];         // ProgTab index: DC first -> DC table per component,
+                          // AC scans -> tab[0] = AC table; -1 if unused
+  int64_t data_off;       // entropy-coded bytes: absolute offset in the data buffer
+  int64_t data_len;       // bytes up to the marker that ends the scan
+};
+
+// Progressive-scan Huffman table for the serial decoder: an 8-bit lookahead
+// (jdhuff.c HUFF_LOOKAHEAD) plus the canonical maxcode/valoffset search.
+struct ProgTab {
+  uint16_t look[256];  // codes <= 8 bits: (length << 8) | symbol; 0 = longer code
+  int32_t maxcode[18]; // [l] largest code of length l (-1 none), [17] sentinel
+  int32_t valoff[18];
+  uint8_t vals[256];
+};
+constexpr int kMaxProgScans = 64; // per image; more -> LDT_IMG_UNSUPPORTED
 
 // Per-batch plan header; offsets are bytes from the start of the plan blob.
 struct PlanHdr {

@@ -31,7 +31,7 @@ IMG_TOO_LARGE = 4
 IMG_NULL = 5
 IMG_STATUS_TEXT = {
     IMG_NOT_JPEG: "cannot identify image file (not a baseline JPEG)",
-    IMG_UNSUPPORTED: "unsupported JPEG (progressive/arithmetic/12-bit/CMYK/multi-scan)",
+    IMG_UNSUPPORTED: "unsupported JPEG (arithmetic/lossless/12-bit/CMYK/multi-scan sequential)",
     IMG_CORRUPT: "image file is truncated or corrupt",
     IMG_TOO_LARGE: "image dimensions exceed LDT_MAX_DIM",
     IMG_NULL: "null image cell",

@@ -401,3 +401,43 @@ def test_pipelined_to_tensor_fn_host_batches():
     with pytest.raises(ldt_amd.ImageDecodeError) as ei:
         fn.check()
     assert set(ei.value.rows) == {1}
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_progressive_mixed_batches_vs_oracle(seed):
+    """SOF2 images (k_prog: jdphuff.c scans) mixed with baseline ones in one
+    batch, random shapes/subsampling/quality/restart intervals, bit-exact
+    against the oracle (which is pinned to Pillow by the progressive goldens)."""
+    import ldt_amd
+    from ldt_amd import synth
+
+    r = np.random.RandomState(100 + seed)
+    cells = []
+    for k in range(12):
+        h, w = int(r.randint(1, 300)), int(r.randint(1, 300))
+        kw = dict(quality=int(r.choice([50, 75, 90, 97])),
+                  subsampling=str(r.choice(["4:2:0", "4:2:2", "4:4:4"])),
+                  progressive=bool(k % 3 != 0))
+        if r.rand() < 0.3:
+            kw["restart_marker_blocks"] = int(r.randint(1, 6))
+        cells.append(synth.encode(synth.field(h, w, int(r.randint(1 << 30)), float(r.choice([0, 6, 30]))), **kw))
+    out = ldt_amd.decode_tensor_image(_batch(cells))
+    img = out["image"].cpu().numpy()
+    for k, b in enumerate(cells):
+        _check(img[k], oracle.jpeg_to_tensor(b), f"seed{seed}[{k}]")
+
+
+def test_progressive_config_sized_batch():
+    """C2-shaped progressive images (512x512 q90 4:2:0) through the same
+    to_tensor_fn: the serial per-scan path at full size, twice (the
+    coefficient buffer stays clean across batches)."""
+    import ldt_amd
+    from ldt_amd import synth
+
+    cells = [synth.encode(synth.field(512, 512, 900 + k, 20), quality=90, progressive=True) for k in range(4)]
+    base, _ = synth.q90_512(4, seed=5)
+    for rep in range(2):
+        batch = cells + list(base) if rep == 0 else list(base) + cells
+        img = ldt_amd.decode_tensor_image(_batch(batch))["image"].cpu().numpy()
+        for k, b in enumerate(batch):
+            _check(img[k], oracle.jpeg_to_tensor(b), f"rep{rep}[{k}]")
