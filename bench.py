@@ -6,7 +6,7 @@ decode, IDCT, fused upsample/colour/Resize(224,224)/ToTensor store, labels.
 Default workload (N=1 and per rank for N>1, weak scaling): BASELINE.json
 configs[1] — 512x512 baseline JPEG, 4:2:0, q90, batch 256 per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c4|c5|c2p]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line. The CPU baseline (rank 0, N=1 only) times the
@@ -37,6 +37,9 @@ WORKLOADS = {
                batch=128),
     "c4": dict(desc="ImageNet-shaped ~500x375 variable JPEG q90 with restart markers (configs[3] data)", batch=128),
     "c5": dict(desc="raw uint8 HWC 1024x1024 -> Resize 224 + Normalize (configs[4])", batch=1024),
+    # not a BASELINE config: the c2 images encoded progressive (SOF2), to
+    # measure the serial per-scan path
+    "c2p": dict(desc="c2's 512x512 q90 4:2:0 images as progressive JPEG (SOF2)", batch=256),
 }
 
 
@@ -45,6 +48,8 @@ def make_cells(workload: str, n: int, seed: int):
 
     if workload == "c2":
         return synth.q90_512(n, seed=seed)
+    if workload == "c2p":
+        return synth.q90_512(n, seed=seed, progressive=True)
     if workload == "c1":
         return synth.food101_like(n, seed=seed)
     if workload == "c4":
@@ -303,12 +308,12 @@ def load_profile(name: str):
 
 
 def ldt_amd_dims(cell: bytes):
-    """(H, W) from the SOF0 marker (host-side helper for byte accounting)."""
+    """(H, W) from the SOF0/1/2 marker (host-side helper for byte accounting)."""
     i = 2
     while i + 4 <= len(cell):
         m = cell[i + 1]
         L = (cell[i + 2] << 8) | cell[i + 3]
-        if m in (0xC0, 0xC1):
+        if m in (0xC0, 0xC1, 0xC2):
             return (cell[i + 5] << 8) | cell[i + 6], (cell[i + 7] << 8) | cell[i + 8]
         i += 2 + L
     raise ValueError("no SOF")

@@ -32,7 +32,10 @@ constexpr int kWin = 16384; // scan bytes staged in LDS
 constexpr int kChunk = 64;  // blocks staged per round (one per lane)
 
 struct ProgLds {
-  uint8_t win[kWin];
+  union {
+    uint8_t win[kWin];
+    uint32_t win32[kWin / 4];
+  };
   __attribute__((aligned(16))) int16_t blk[kChunk][64]; // zigzag slots; [0] unused
   int16_t dc[kChunk];
   int64_t bidx[kChunk]; // coefficient-buffer block index of each staged slot
@@ -46,25 +49,52 @@ struct ProgLds {
 struct PReader {
   const uint8_t *data;
   int64_t pos, lim; // lim: one past the marker that ends the scan
+  int64_t wb, wl;   // the LDS window's data range (copied from ProgLds)
   uint64_t buf;
   int bits;
   int marker; // 0: none yet; else the marker code reached
 };
 
-__device__ __forceinline__ int pbyte(const ProgLds &L, const uint8_t *data, int64_t p) {
-  const int64_t o = p - L.win_base;
-  return (o >= 0 && p < L.win_lim) ? L.win[o] : data[p];
+__device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int64_t p) {
+  int v;
+  if (p < r.wl) v = L.win[(int)(p - r.wb)];
+  else v = __builtin_nontemporal_load(r.data + p);
+  return v;
 }
 
+// Appends whole bytes while at most 56 bits are buffered. Fast path: the next
+// 8 window bytes hold no 0xFF (no stuffing, no marker) -> one read of three
+// aligned LDS words instead of a dependent read per byte.
 __device__ __forceinline__ void pfill(PReader &r, const ProgLds &L) {
+  if (r.marker == 0 && r.pos + 12 <= r.wl) {
+    const int o = (int)(r.pos - r.wb);
+    const uint32_t a = L.win32[o >> 2], b = L.win32[(o >> 2) + 1], c = L.win32[(o >> 2) + 2];
+    const uint32_t sh = (uint32_t)(o & 3) * 8;
+    // bytes pos..pos+7 in memory order, little-endian words
+    const uint32_t lo = sh ? (a >> sh) | (b << (32 - sh)) : a;
+    const uint32_t hi = sh ? (b >> sh) | (c << (32 - sh)) : b;
+    // any 0xFF byte among the 8?
+    const uint32_t xl = ~lo, xh = ~hi;
+    const uint32_t ffm = ((xl - 0x01010101u) & ~xl & 0x80808080u) | ((xh - 0x01010101u) & ~xh & 0x80808080u);
+    if (ffm == 0) {
+      const int nb = (64 - r.bits) >> 3; // bytes that fit
+      // big-endian bit order: byte i of memory goes to bits 56-8i of the word
+      const uint64_t be = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+      const uint64_t keep = nb == 8 ? ~0ull : ~(~0ull >> (8 * nb));
+      r.buf |= (be & keep) >> r.bits;
+      r.bits += 8 * nb;
+      r.pos += nb;
+      return;
+    }
+  }
   while (r.bits <= 56) {
     int c = 0;
     if (r.marker == 0 && r.pos < r.lim) {
-      c = pbyte(L, r.data, r.pos++);
+      c = pbyte(r, L, r.pos++);
       if (c == 0xFF) {
         int c2;
         do {
-          c2 = r.pos < r.lim ? pbyte(L, r.data, r.pos++) : 0x100;
+          c2 = r.pos < r.lim ? pbyte(r, L, r.pos++) : 0x100;
         } while (c2 == 0xFF);
         if (c2 == 0) {
           c = 0xFF;
@@ -126,7 +156,7 @@ __device__ __forceinline__ void prestart(PReader &r, const ProgLds &L) {
   }
   if (r.marker != 0) return; // another marker: zero bits for the rest of the scan
   while (r.pos + 1 < r.lim) {
-    const int a = pbyte(L, r.data, r.pos), b = pbyte(L, r.data, r.pos + 1);
+    const int a = pbyte(r, L, r.pos), b = pbyte(r, L, r.pos + 1);
     if (a == 0xFF && b >= 0xD0 && b <= 0xD7) {
       r.pos += 2;
       return;
@@ -256,6 +286,8 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
       }
       __syncthreads();
       if (lane == 0) {
+        R.wb = L.win_base;
+        R.wl = L.win_lim;
         int slot = 0;
         for (int ui = 0; ui < nu; ++ui) {
           if (sc.restart) {

@@ -49,9 +49,12 @@ def food101_like(n: int, seed: int = 0, noise: float = 6.0) -> Tuple[List[bytes]
     return cells, np.arange(n, dtype=np.int64) % 101
 
 
-def q90_512(n: int, seed: int = 0, noise: float = 6.0) -> Tuple[List[bytes], np.ndarray]:
-    """Config 2: 512x512 baseline, 4:2:0, quality 90, no DRI."""
-    cells = [encode(field(512, 512, seed * 100003 + i, noise), quality=90, subsampling="4:2:0")
+def q90_512(n: int, seed: int = 0, noise: float = 6.0,
+            progressive: bool = False) -> Tuple[List[bytes], np.ndarray]:
+    """Config 2: 512x512 baseline, 4:2:0, quality 90, no DRI (progressive=True:
+    the same images as SOF2, libjpeg's default progression script)."""
+    cells = [encode(field(512, 512, seed * 100003 + i, noise), quality=90, subsampling="4:2:0",
+                    progressive=progressive)
              for i in range(n)]
     return cells, np.arange(n, dtype=np.int64) % 101
 
