@@ -174,6 +174,22 @@ int ldt_shard_fragments(ldt_ctx *ctx, const int64_t *fragment_rows_dev, int nfra
                         int64_t *out_dev, int64_t capacity, int64_t *out_count_dev,
                         int64_t *out_local_count_dev, void *stream);
 
+/* torch.utils.data.DistributedSampler index computation, on device — the
+ * map-style loader's sampler (lance_map_style.py:58 -> torch 2.10
+ * torch/utils/data/distributed.py:94-103 (num_samples) and :107-141 (__iter__)).
+ * Writes the rank's num_samples indices (int64) into out_dev (capacity
+ * entries) and num_samples into *num_samples_out (host, may be NULL):
+ *   perm = torch.randperm(dataset_len, generator=manual_seed(seed)) when
+ *   shuffle != 0 (bit-exact: MT19937 seeded with the low 32 bits of the 64-bit
+ *   torch seed, forward Fisher-Yates), else the identity; padded by wrapping
+ *   (drop_last == 0) or truncated; then every num_replicas-th from rank.
+ * `seed` is the sampler's seed + epoch as torch's uint64 seed (two's complement
+ * for negative values). dataset_len must be < 2^32/20 (torch draws 64-bit
+ * numbers beyond that). */
+int ldt_distributed_indices(ldt_ctx *ctx, int64_t dataset_len, int num_replicas, int rank,
+                            int shuffle, uint64_t seed, int drop_last, int64_t *out_dev,
+                            int64_t capacity, int64_t *num_samples_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

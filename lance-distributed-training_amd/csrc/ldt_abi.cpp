@@ -530,6 +530,7 @@ struct ldt_ctx {
   int debug_skip = 0; // LDT_OPT_DEBUG_SKIP
   int subseq_bits = 1024;
   DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_sub, d_pre, d_dscnt;
+  DevBuf d_perm; // DistributedSampler scratch: 3 int32 arrays of dataset_len
   bool coef_dirty = false; // a batch wrote coefficients but k_idct did not run
   std::unique_ptr<CopyPool> copier; // host -> pinned copies (created on first use)
   static constexpr int kSlots = 2;
@@ -1430,6 +1431,49 @@ int ldt_shard_fragments(ldt_ctx *c, const int64_t *fragment_rows_dev, int nfrag,
   HIPCHK(c, launch_shard_fragments(fragment_rows_dev, nfrag, batch_size, rank, world_size, pad_to,
                                    out_dev, capacity, out_count_dev, out_local_count_dev,
                                    (hipStream_t)stream));
+  return LDT_OK;
+}
+
+// torch.utils.data.DistributedSampler.__iter__ (distributed.py:107-141) on
+// device: randperm (n < 2^32/20, torch's MT19937 Fisher-Yates branch), pad by
+// wrapping or truncate (drop_last), stride by rank. num_samples as :94-103.
+int ldt_distributed_indices(ldt_ctx *c, int64_t dataset_len, int num_replicas, int rank,
+                            int shuffle, uint64_t seed, int drop_last, int64_t *out_dev,
+                            int64_t capacity, int64_t *num_samples_out, void *stream) {
+  if (!c) return LDT_ERR_ARG;
+  if (dataset_len < 0 || num_replicas <= 0 || rank < 0 || rank >= num_replicas ||
+      (capacity > 0 && !out_dev))
+    return set_err(c, LDT_ERR_ARG, "bad distributed_indices arguments");
+  if (dataset_len >= (int64_t)(UINT32_MAX / 20))
+    return set_err(c, LDT_ERR_ARG,
+                   "dataset_len %lld >= 2^32/20: torch.randperm switches to 64-bit draws",
+                   (long long)dataset_len);
+  const int64_t n = dataset_len, W = num_replicas;
+  int64_t num_samples;
+  if (drop_last && n % W != 0) {
+    // math.ceil((n - W) / W) with true division (n - W may be negative)
+    const int64_t a = n - W;
+    num_samples = a >= 0 ? (a + W - 1) / W : -((-a) / W);
+  } else {
+    num_samples = (n + W - 1) / W;
+  }
+  if (num_samples < 0) num_samples = 0;
+  if (num_samples_out) *num_samples_out = num_samples;
+  if (num_samples == 0) return LDT_OK;
+  if (capacity < num_samples)
+    return set_err(c, LDT_ERR_ARG, "capacity %lld < num_samples %lld", (long long)capacity,
+                   (long long)num_samples);
+  DeviceGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (shuffle) {
+    int rc;
+    if ((rc = ensure_dev(c, c->d_perm, (size_t)n * 4 * 3 + 64, s))) return rc;
+    int32_t *base = static_cast<int32_t *>(c->d_perm.p);
+    HIPCHK(c, launch_dist_shuffled((uint32_t)(seed & 0xffffffffu), n, rank, num_replicas,
+                                   num_samples, base, base + n, base + 2 * n, out_dev, s));
+  } else {
+    HIPCHK(c, launch_dist_select(nullptr, n, rank, num_replicas, num_samples, out_dev, s));
+  }
   return LDT_OK;
 }
 

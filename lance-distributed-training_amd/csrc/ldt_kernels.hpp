@@ -90,5 +90,13 @@ hipError_t launch_shard_ranges(int64_t num_rows, int64_t bsz, int rank, int worl
 hipError_t launch_shard_fragments(const int64_t *frag_rows, int nfrag, int64_t bsz, int rank,
                                   int world, int64_t pad_to, int64_t *out, int64_t capacity,
                                   int64_t *count, int64_t *local_count, hipStream_t s);
+// DistributedSampler indices (ldt_sampler.hip). Shuffled: the rank's
+// num_samples entries of torch.randperm(n) strided from rank (H, head, nxt: n
+// int32 each of scratch). launch_dist_select: the unshuffled identity.
+hipError_t launch_dist_shuffled(uint32_t seed, int64_t n, int rank, int world,
+                                int64_t num_samples, int32_t *H, int32_t *head, int32_t *nxt,
+                                int64_t *out, hipStream_t s);
+hipError_t launch_dist_select(const int32_t *perm, int64_t n, int rank, int world,
+                              int64_t num_samples, int64_t *out, hipStream_t s);
 
 } // namespace ldt

@@ -11,7 +11,7 @@ All decode/resize/shard arithmetic runs in libldt.so's gfx950 HIP kernels.
 from ._lib import ImageDecodeError, LdtError, load_library, version  # noqa: F401
 from .dataset import (ArrowDataset, LanceDataset, SafeLanceDataset, dataset,  # noqa: F401
                       get_safe_loader, write_dataset)
-from .sampler import FullScanSampler, ShardedBatchSampler, ShardedFragmentSampler  # noqa: F401
+from .sampler import DistributedSampler, FullScanSampler, ShardedBatchSampler, ShardedFragmentSampler  # noqa: F401
 from .transforms import (IMAGENET_MEAN, IMAGENET_STD, DecodePipeline, ResidentBatch, collate_fn,  # noqa: F401
                          decode_arrow, decode_tensor_image, make_collate_fn, make_to_tensor_fn,
                          resize_raw)

@@ -53,7 +53,7 @@ EXPORTED = (
     "ldt_create", "ldt_destroy", "ldt_last_error", "ldt_set_option", "ldt_version",
     "ldt_decode_batch", "ldt_decode_batch_large", "ldt_decode_batch_resident",
     "ldt_fetch_status", "ldt_stage_times", "ldt_resize_raw", "ldt_shard_ranges",
-    "ldt_shard_fragments",
+    "ldt_shard_fragments", "ldt_distributed_indices",
 )
 
 
@@ -115,11 +115,14 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_resize_raw.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, vp, vp]
         L.ldt_shard_ranges.argtypes = [vp, i64, i64, i32, i32, vp, i64, vp, vp]
         L.ldt_shard_fragments.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, i64, vp, vp, vp]
+        L.ldt_distributed_indices.argtypes = [vp, i64, i32, i32, i32, ctypes.c_uint64, i32, vp, i64,
+                                              vp, vp]
         L.ldt_debug_resample_coeffs.argtypes = [vp, i32, i32, vp, vp, vp]
         L.ldt_debug_counters.argtypes = [vp, vp, vp]
         for name in ("ldt_set_option", "ldt_decode_batch", "ldt_decode_batch_large",
                      "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_resize_raw", "ldt_stage_times",
-                     "ldt_shard_ranges", "ldt_shard_fragments", "ldt_debug_resample_coeffs",
+                     "ldt_shard_ranges", "ldt_shard_fragments", "ldt_distributed_indices",
+                     "ldt_debug_resample_coeffs",
                      "ldt_debug_counters"):
             getattr(L, name).restype = ctypes.c_int
         _lib = L

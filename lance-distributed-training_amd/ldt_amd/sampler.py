@@ -16,6 +16,11 @@ and pylance's ``lance.sampler`` classes:
   re-yields its own batches cyclically; a rank that owns no rows cycles the
   global batch list from index ``rank``.
 * ``FullScanSampler()`` — every fragment, every rank (README.md:130-138).
+* ``DistributedSampler(dataset, num_replicas, rank, shuffle, seed, drop_last)``
+  — the map-style loader's sampler (lance_map_style.py:58), torch's
+  ``torch/utils/data/distributed.py:66-157`` with the index computation
+  (randperm, pad/truncate, rank stride) in the ``ldt_distributed_indices``
+  kernels, bit-exact with torch.
 
 The per-rank ranges are computed by libldt.so's device kernels
 (``ldt_shard_ranges`` / ``ldt_shard_fragments``). Samplers are called as
@@ -79,6 +84,23 @@ def device_fragment_batches(fragment_rows: Sequence[int], batch_size: int, rank:
                                           s.cuda_stream), "ldt_shard_fragments")
     n = int(cnt.item())
     return [tuple(r) for r in out[:n].cpu().tolist()], int(local.item())
+
+
+def device_distributed_indices(n: int, num_replicas: int, rank: int, shuffle: bool, seed: int,
+                               drop_last: bool) -> torch.Tensor:
+    """The rank's DistributedSampler indices as an int64 device tensor, from
+    the ``ldt_distributed_indices`` kernels (``seed`` = sampler seed + epoch)."""
+    dev = _device()
+    ctx = _lib.get_context(dev.index)
+    cap = max(1, -(-n // num_replicas))
+    out = torch.empty((cap,), dtype=torch.int64, device=dev)
+    ns = ctypes.c_int64(0)
+    s = torch.cuda.current_stream(dev)
+    ctx.check(ctx.lib.ldt_distributed_indices(ctx.handle, n, num_replicas, rank, int(bool(shuffle)),
+                                              int(seed) % (1 << 64), int(bool(drop_last)),
+                                              out.data_ptr(), cap, ctypes.byref(ns), s.cuda_stream),
+              "ldt_distributed_indices")
+    return out[: ns.value]
 
 
 def agree_max(value: int, group=None) -> int:
@@ -183,3 +205,60 @@ class FullScanSampler(_SamplerBase):
             n = frag.count_rows()
             for s in range(0, n, batch_size):
                 yield frag.read_slice(s, min(s + batch_size, n), columns=columns)
+
+
+class DistributedSampler(torch.utils.data.Sampler):
+    """``torch.utils.data.DistributedSampler`` (distributed.py:66-157) with the
+    index computation on the GPU — same constructor, ``set_epoch``, ``__len__``
+    and iteration order. ``indices()`` returns the rank's indices as a device
+    tensor (no host round trip) for loaders that gather on device."""
+
+    def __init__(self, dataset, num_replicas: Optional[int] = None, rank: Optional[int] = None,
+                 shuffle: bool = True, seed: int = 0, drop_last: bool = False,
+                 compute: Optional[Callable] = None) -> None:
+        import math
+
+        import torch.distributed as dist
+
+        if num_replicas is None:
+            if not dist.is_available():
+                raise RuntimeError("Requires distributed package to be available")
+            num_replicas = dist.get_world_size()
+        if rank is None:
+            if not dist.is_available():
+                raise RuntimeError("Requires distributed package to be available")
+            rank = dist.get_rank()
+        if rank >= num_replicas or rank < 0:
+            raise ValueError(f"Invalid rank {rank}, rank should be in the interval [0, {num_replicas - 1}]")
+        self.dataset = dataset
+        self.num_replicas = num_replicas
+        self.rank = rank
+        self.epoch = 0
+        self.drop_last = drop_last
+        if self.drop_last and len(self.dataset) % self.num_replicas != 0:
+            self.num_samples = math.ceil((len(self.dataset) - self.num_replicas) / self.num_replicas)
+        else:
+            self.num_samples = math.ceil(len(self.dataset) / self.num_replicas)
+        self.total_size = self.num_samples * self.num_replicas
+        self.shuffle = shuffle
+        self.seed = seed
+        self.compute = compute or device_distributed_indices
+
+    def indices(self):
+        """The rank's indices for the current epoch (device tensor on the GPU path)."""
+        return self.compute(len(self.dataset), self.num_replicas, self.rank, self.shuffle,
+                            self.seed + self.epoch, self.drop_last)
+
+    def __iter__(self):
+        idx = self.indices()
+        idx = idx.tolist() if hasattr(idx, "tolist") else list(idx)
+        if len(idx) != self.num_samples:
+            raise AssertionError(f"Number of subsampled indices ({len(idx)}) does not match "
+                                 f"num_samples ({self.num_samples})")
+        return iter(idx)
+
+    def __len__(self) -> int:
+        return self.num_samples
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = epoch

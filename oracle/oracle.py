@@ -23,9 +23,11 @@ Contents
 from __future__ import annotations
 
 import ctypes
+import functools
 import io
+import math
 import os
-from typing import Sequence
+from typing import List, Sequence
 
 import numpy as np
 
@@ -253,3 +255,78 @@ def sharded_fragment_batches(fragment_rows: Sequence[int], batch_size: int, rank
             res.append((ff, s, e, g, 1))
             i += 1
     return res
+
+
+# ---------------------------------------------------------------------------
+# Map-style DistributedSampler (lance_map_style.py:58 -> torch 2.10
+# torch/utils/data/distributed.py:94-141). Pinned against torch itself in
+# tests/test_oracle.py (torch.randperm / DistributedSampler are in-container).
+# ---------------------------------------------------------------------------
+def mt19937_u32(seed: int, count: int) -> np.ndarray:
+    """MT19937 32-bit outputs (torch CPUGeneratorImpl::random(): the engine is
+    seeded with the low 32 bits of the 64-bit seed). Vectorised twist."""
+    N, M = 624, 397
+    st = np.zeros(N, np.uint64)
+    v = seed & 0xFFFFFFFF
+    st[0] = v
+    for j in range(1, N):
+        v = (1812433253 * (v ^ (v >> 30)) + j) & 0xFFFFFFFF
+        st[j] = v
+    st = st.astype(np.uint32)
+    out = np.empty(max(count, 0), np.uint32)
+    pos = 0
+    mag = np.array([0, 0x9908B0DF], np.uint32)
+    while pos < count:
+        new = np.empty(N, np.uint32)
+        k = np.arange(N - M)
+        y = (st[k] & 0x80000000) | (st[k + 1] & 0x7FFFFFFF)
+        new[k] = st[k + M] ^ (y >> 1) ^ mag[y & 1]
+        k = np.arange(N - M, 2 * (N - M))
+        y = (st[k] & 0x80000000) | (st[k + 1] & 0x7FFFFFFF)
+        new[k] = new[k - (N - M)] ^ (y >> 1) ^ mag[y & 1]
+        k = np.arange(2 * (N - M), N)
+        nxt = np.where(k + 1 < N, st[np.minimum(k + 1, N - 1)], new[0])
+        y = (st[k] & 0x80000000) | (nxt & 0x7FFFFFFF)
+        new[k] = new[k - (N - M)] ^ (y >> 1) ^ mag[y & 1]
+        st = new
+        y = st.copy()
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9D2C5680
+        y ^= (y << 15) & 0xEFC60000
+        y ^= y >> 18
+        take = min(N, count - pos)
+        out[pos:pos + take] = y[:take]
+        pos += take
+    return out
+
+
+@functools.lru_cache(maxsize=8)
+def randperm(n: int, seed: int) -> np.ndarray:
+    """torch.randperm(n, generator=manual_seed(seed)) for n < 2^32/20: forward
+    Fisher-Yates, z = mt() % (n - i), swap(r[i], r[i + z]) (ATen randperm_cpu)."""
+    r = np.arange(n, dtype=np.int64)
+    z = mt19937_u32(seed, n - 1).astype(np.int64)
+    for i in range(n - 1):
+        k = i + int(z[i] % (n - i))
+        r[i], r[k] = r[k], r[i]
+    r.setflags(write=False)
+    return r
+
+
+def distributed_num_samples(n: int, num_replicas: int, drop_last: bool) -> int:
+    """distributed.py:94-102."""
+    if drop_last and n % num_replicas != 0:
+        return max(0, math.ceil((n - num_replicas) / num_replicas))
+    return math.ceil(n / num_replicas)
+
+
+def distributed_indices(n: int, num_replicas: int, rank: int, shuffle: bool = True,
+                        seed: int = 0, epoch: int = 0, drop_last: bool = False) -> List[int]:
+    """DistributedSampler.__iter__ (distributed.py:107-141)."""
+    base = randperm(n, (seed + epoch) % (1 << 64)) if shuffle else np.arange(n, dtype=np.int64)
+    ns = distributed_num_samples(n, num_replicas, drop_last)
+    total = ns * num_replicas
+    if total == 0:
+        return []
+    p = (rank + np.arange(ns, dtype=np.int64) * num_replicas) % n
+    return base[p].tolist()

@@ -441,3 +441,47 @@ def test_progressive_config_sized_batch():
         img = ldt_amd.decode_tensor_image(_batch(batch))["image"].cpu().numpy()
         for k, b in enumerate(batch):
             _check(img[k], oracle.jpeg_to_tensor(b), f"rep{rep}[{k}]")
+
+
+def test_distributed_sampler_kernels_vs_torch_golden():
+    """ldt_distributed_indices (MT19937 targets, deterministic-reservation
+    Fisher-Yates, rank stride) vs torch's DistributedSampler: every golden case
+    (tests/golden/distributed.json, incl. FOOD101 75,750 rows and ImageNet
+    1,281,167 rows), bit-exact int64 indices."""
+    import json
+    import os
+
+    from ldt_amd.sampler import device_distributed_indices
+
+    cases = json.load(open(os.path.join(GOLDEN, "distributed.json")))["cases"]
+    for g in cases:
+        c = g["case"]
+        for r, exp in enumerate(g["ranks"]):
+            idx = device_distributed_indices(c["n"], c["W"], r, c["shuffle"], c["seed"] + c["epoch"],
+                                             c["drop_last"]).cpu().numpy()
+            assert idx.dtype == np.int64 and len(idx) == exp["count"], c
+            assert sha(idx) == exp["sha256"], (c, r, idx[:4].tolist(), exp["head"])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_distributed_sampler_random_sizes_vs_torch(seed):
+    import torch
+    from torch.utils.data import DistributedSampler as TorchDS
+
+    import ldt_amd
+
+    rng = np.random.default_rng(seed)
+    for _ in range(6):
+        n = int(rng.integers(0, 300_000))
+        W = int(rng.integers(1, 9))
+        dl = bool(rng.integers(0, 2))
+        s = int(rng.integers(-2**62, 2**62))
+        ds = range(n)
+        r = int(rng.integers(0, W))
+        a = ldt_amd.DistributedSampler(ds, num_replicas=W, rank=r, seed=s, drop_last=dl)
+        b = TorchDS(ds, num_replicas=W, rank=r, seed=s, drop_last=dl)
+        a.set_epoch(seed)
+        b.set_epoch(seed)
+        assert list(a) == list(b), (n, W, r, dl, s)
+        t = a.indices()
+        assert t.is_cuda and t.dtype == torch.int64

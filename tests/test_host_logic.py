@@ -91,3 +91,39 @@ def test_image_decode_error_is_oserror_and_valueerror():
     e = ImageDecodeError({3: 1, 0: 3})
     assert isinstance(e, OSError) and isinstance(e, ValueError)
     assert "row 0" in str(e) and "row 3" in str(e)
+
+
+def _dist_compute(n, W, r, shuffle, seed, drop_last):
+    # the oracle stands in for the device kernel (checker only)
+    return np.asarray(oracle.distributed_indices(n, W, r, shuffle, seed, 0, drop_last), np.int64)
+
+
+@pytest.mark.parametrize("n,W,drop_last", [(10, 3, False), (10, 3, True), (1, 4, False), (1, 4, True),
+                                           (257, 8, False), (0, 2, False)])
+def test_distributed_sampler_host_logic_matches_torch(n, W, drop_last):
+    """ldt_amd.DistributedSampler: constructor, num_samples, set_epoch and
+    iteration order identical to torch's (distributed.py:66-157)."""
+    from torch.utils.data import DistributedSampler as TorchDS
+
+    from ldt_amd import DistributedSampler
+
+    ds = list(range(n))
+    for r in range(W):
+        for shuffle in (True, False):
+            a = DistributedSampler(ds, num_replicas=W, rank=r, shuffle=shuffle, seed=5, drop_last=drop_last,
+                                   compute=_dist_compute)
+            b = TorchDS(ds, num_replicas=W, rank=r, shuffle=shuffle, seed=5, drop_last=drop_last)
+            for ep in (0, 2):
+                a.set_epoch(ep)
+                b.set_epoch(ep)
+                assert len(a) == len(b) and a.total_size == b.total_size
+                assert list(a) == list(b)
+
+
+def test_distributed_sampler_rank_errors():
+    from ldt_amd import DistributedSampler
+
+    with pytest.raises(ValueError):
+        DistributedSampler(range(5), num_replicas=2, rank=2)
+    with pytest.raises(ValueError):
+        DistributedSampler(range(5), num_replicas=2, rank=-1)

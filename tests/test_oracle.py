@@ -3,11 +3,13 @@ outputs) and against Pillow directly on seeded inputs; sampler restatement
 against the FOOD101 arithmetic of README.md:164-191."""
 import hashlib
 import io
+import json
+import os
 
 import numpy as np
 import pytest
 
-from conftest import read_golden
+from conftest import GOLDEN, read_golden
 from oracle import oracle
 
 
@@ -109,3 +111,30 @@ def test_readme_deadlock_arithmetic():
     # W=8: rank 7 owns no rows, padded to 98
     assert len(oracle.sharded_fragment_batches(F, 128, 7, 8)) == 0
     assert len(oracle.sharded_fragment_batches(F, 128, 7, 8, pad=True)) == 98
+
+
+def _distributed_golden():
+    return json.load(open(os.path.join(GOLDEN, "distributed.json")))["cases"]
+
+
+def test_distributed_sampler_oracle_matches_torch_golden():
+    """oracle.distributed_indices (MT19937 + Fisher-Yates restatement) vs the
+    sha256 of torch's own DistributedSampler output (tests/golden/distributed.json)."""
+    for g in _distributed_golden():
+        c = g["case"]
+        if c["n"] > 100_000:
+            continue  # the 1.28M case is checked on the GPU path only (pure-Python loop)
+        for r, exp in enumerate(g["ranks"]):
+            idx = np.asarray(oracle.distributed_indices(c["n"], c["W"], r, c["shuffle"], c["seed"],
+                                                        c["epoch"], c["drop_last"]), np.int64)
+            assert len(idx) == exp["count"] == oracle.distributed_num_samples(c["n"], c["W"], c["drop_last"])
+            assert hashlib.sha256(idx.tobytes()).hexdigest() == exp["sha256"], c
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (53, 7), (4096, 2**33 + 5), (30000, -9)])
+def test_randperm_restatement_vs_torch(n, seed):
+    import torch
+
+    g = torch.Generator()
+    g.manual_seed(seed)
+    assert torch.randperm(n, generator=g).tolist() == oracle.randperm(n, seed % (1 << 64)).tolist()
