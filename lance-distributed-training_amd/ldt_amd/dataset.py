@@ -172,9 +172,15 @@ class LanceDataset(IterableDataset):
         from .sampler import FullScanSampler
 
         sampler = self.sampler or FullScanSampler()
-        for rb in sampler(self.dataset, batch_size=self.batch_size, columns=self.columns,
-                          filter=self.filter, batch_readahead=self.batch_readahead):
-            yield self.to_tensor_fn(rb) if self.to_tensor_fn is not None else rb
+        batches = sampler(self.dataset, batch_size=self.batch_size, columns=self.columns,
+                          filter=self.filter, batch_readahead=self.batch_readahead)
+        fn = self.to_tensor_fn
+        if fn is not None and getattr(fn, "prefetch", 0) > 0:
+            # make_to_tensor_fn(prefetch=k): decode k batches ahead on side streams
+            yield from fn.iterate(batches)
+            return
+        for rb in batches:
+            yield fn(rb) if fn is not None else rb
 
 
 class SafeLanceDataset(Dataset):

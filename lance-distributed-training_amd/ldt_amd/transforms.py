@@ -316,11 +316,18 @@ class DecodePipeline:
         self.sizes = [0] * self.depth
         self.k = 0
 
-    def decode(self, batch, normalize=None, image_column: str = "image", label_column: str = "label"):
+    def decode(self, batch, normalize=None, image_column: str = "image", label_column: str = "label",
+               wait: bool = True):
         """Enqueue one batch: a ``ResidentBatch`` (cells already in HBM) or a
         host ``pa.RecordBatch`` as LanceDataset yields it (its buffers are
         copied into the slot's pinned ring during the call, then to HBM
-        asynchronously on the slot's stream)."""
+        asynchronously on the slot's stream).
+
+        ``wait=True``: torch's current stream waits for the result now;
+        returns ``(image, label)``. ``wait=False``: nothing waits yet; returns
+        ``(image, label, ready)`` and the consumer calls ``ready()`` on the
+        stream that will use the tensors, so work enqueued there in between
+        (a training step) overlaps this decode (see ``prefetch``)."""
         slot = self.k % self.depth
         self.k += 1
         s = self.streams[slot]
@@ -340,11 +347,56 @@ class DecodePipeline:
             decode_arrow(images, lab, device=self.dec.device, normalize=normalize, stream=s,
                          ctx=self.ctxs[slot], out=out, out_lbl=lbl)
         self.sizes[slot] = n
-        cur.wait_stream(s)
-        out.record_stream(cur)
-        if lbl is not None:
-            lbl.record_stream(cur)
-        return out, lbl
+        if wait:
+            cur.wait_stream(s)
+            out.record_stream(cur)
+            if lbl is not None:
+                lbl.record_stream(cur)
+            return out, lbl
+        ev = torch.cuda.Event()
+        ev.record(s)
+
+        def ready():
+            use = torch.cuda.current_stream(self.dec.device)
+            use.wait_event(ev)
+            out.record_stream(use)
+            if lbl is not None:
+                lbl.record_stream(use)
+
+        return out, lbl, ready
+
+    def prefetch(self, batches, ahead: int = 2, normalize=None, image_column: str = "image",
+                 label_column: str = "label"):
+        """Iterate ``batches`` (host RecordBatches or ResidentBatches) yielding
+        ``{"image", "label"}`` dicts, with the decode of the next ``ahead``
+        batches enqueued before each yield: while the consumer's step k runs on
+        torch's stream, batches k+1..k+ahead decode on the slots' streams
+        (decode overlapped with the training step, so
+        ``.to(device)`` at lance_iterable.py:108-109 is a no-op). Per-image
+        errors surface when a slot is reused or at the end."""
+        from collections import deque
+
+        ahead = max(0, min(int(ahead), self.depth - 1))
+        q = deque()
+
+        def emit():
+            img, lbl, ready = q.popleft()
+            ready()
+            out = {"image": img}
+            if lbl is not None:
+                out["label"] = lbl
+            return out
+
+        for b in batches:
+            if self.k >= self.depth:
+                self.check_slot(self.k % self.depth)
+            q.append(self.decode(b, normalize=normalize, image_column=image_column,
+                                 label_column=label_column, wait=False))
+            if len(q) > ahead:
+                yield emit()
+        while q:
+            yield emit()
+        self.check()
 
     def stage_times(self, reset: bool = False):
         tot: dict = {}
@@ -379,14 +431,18 @@ class DecodePipeline:
             raise ImageDecodeError(bad)
 
 
-def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, **fixed):
+def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int = 0, **fixed):
     """A pipelined ``to_tensor_fn`` for ``LanceDataset(..., to_tensor_fn=...)``
     (lance_iterable.py:53-59): each call enqueues its RecordBatch on one of
     `depth` contexts/streams and returns at once, so batch k+1's host copy and
     kernels overlap batch k's. The tensors are ready on torch's current stream
     (it waits for the slot's stream). Per-image errors are reported
     asynchronously: by ``fn.check()``, and at the latest when a slot is reused
-    (`depth` calls later) — unlike the synchronous ``decode_tensor_image``."""
+    (`depth` calls later) — unlike the synchronous ``decode_tensor_image``.
+
+    ``prefetch=k`` (k < depth): ``LanceDataset`` iterates through
+    ``fn.iterate`` instead, enqueueing the next k batches before yielding each
+    one, so their decode overlaps the consumer's training step."""
     pipe = DecodePipeline(depth=depth, device=device)
 
     def to_tensor_fn(batch, **kwargs):
@@ -402,4 +458,8 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, **fixed):
 
     to_tensor_fn.check = pipe.check
     to_tensor_fn.pipeline = pipe
+    to_tensor_fn.prefetch = max(0, min(int(prefetch), depth - 1))
+    to_tensor_fn.iterate = lambda batches: pipe.prefetch(
+        batches, ahead=to_tensor_fn.prefetch, normalize=normalize,
+        image_column=fixed.get("image_column", "image"), label_column=fixed.get("label_column", "label"))
     return to_tensor_fn
