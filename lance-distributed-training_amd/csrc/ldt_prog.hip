@@ -6,12 +6,14 @@
 // buffer the baseline decoder fills (zigzag slots 1..63 in `coef`, the final
 // DC value in `dcv`), so k_idct and the resize kernels then run unchanged.
 //
-// One 64-lane workgroup per progressive image. A scan's Huffman decode is a
-// serial bit stream, so lane 0 decodes while the other lanes stage its
+// Four 64-lane workgroups per progressive image, one per independent scan
+// chain (DC scans; each component's AC scans). A scan's Huffman decode is a
+// serial bit stream: the wave decodes it with wave-uniform (scalar) state
+// (lane 0 stores) between chunks in which all lanes stage its
 // inputs: the scan's bytes in an LDS window, and the coefficients of the next
 // 64 blocks (one block per lane, coalesced 16-byte loads) which lane 0 then
-// reads and refines in LDS before the wave writes them back. Scans run in
-// file order (a refinement scan depends on the earlier scans of its band).
+// reads and refines in LDS before the wave writes them back. A chain's scans
+// run in file order (a refinement scan depends on the earlier scans of its band).
 //
 // Reference semantics: libjpeg-turbo jdphuff.c (Pillow 12.2.0's decoder),
 // jdhuff.c jpeg_fill_bit_buffer (byte stuffing, zero bits at a marker),
@@ -39,6 +41,8 @@ struct ProgLds {
   __attribute__((aligned(16))) int16_t blk[kChunk][64]; // zigzag slots; [0] unused
   int16_t dc[kChunk];
   int64_t bidx[kChunk]; // coefficient-buffer block index of each staged slot
+  uint64_t nzm[kChunk];  // AC refinement: zigzag positions nonzero before the scan
+  uint64_t corr[kChunk]; // AC refinement: positions whose correction bit is 1
   ProgTab tabs[4];
   int64_t win_base, win_lim; // data offsets of win[0] and one past its last valid byte
   int64_t pos;               // lane 0's reader position (for window refills)
@@ -55,11 +59,20 @@ struct PReader {
   int marker; // 0: none yet; else the marker code reached
 };
 
+// The whole wave runs the decoder with identical values; every value read
+// from LDS or memory passes through readfirstlane, so the compiler keeps the
+// reader state in SGPRs and the control flow on scalar branches (no exec-mask
+// bookkeeping per branch, SALU 64-bit shifts). Stores are made by lane 0.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
 __device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int64_t p) {
   int v;
   if (p < r.wl) v = L.win[(int)(p - r.wb)];
   else v = __builtin_nontemporal_load(r.data + p);
-  return v;
+  return (int)uni((uint32_t)v);
 }
 
 // Appends whole bytes while at most 56 bits are buffered. Fast path: the next
@@ -68,7 +81,8 @@ __device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int64_t
 __device__ __forceinline__ void pfill(PReader &r, const ProgLds &L) {
   if (r.marker == 0 && r.pos + 12 <= r.wl) {
     const int o = (int)(r.pos - r.wb);
-    const uint32_t a = L.win32[o >> 2], b = L.win32[(o >> 2) + 1], c = L.win32[(o >> 2) + 2];
+    const uint32_t a = uni(L.win32[o >> 2]), b = uni(L.win32[(o >> 2) + 1]),
+                   c = uni(L.win32[(o >> 2) + 2]);
     const uint32_t sh = (uint32_t)(o & 3) * 8;
     // bytes pos..pos+7 in memory order, little-endian words
     const uint32_t lo = sh ? (a >> sh) | (b << (32 - sh)) : a;
@@ -121,7 +135,7 @@ __device__ __forceinline__ int pget(PReader &r, const ProgLds &L, int n) {
 // jdhuff.c jpeg_huff_decode: 8-bit lookahead, then the canonical search.
 __device__ __forceinline__ int phuff(PReader &r, const ProgLds &L, const ProgTab &t) {
   if (r.bits < 16) pfill(r, L);
-  const uint32_t e = t.look[r.buf >> 56];
+  const uint32_t e = uni(t.look[r.buf >> 56]);
   if (e) {
     const int l = (int)(e >> 8);
     r.buf <<= l;
@@ -131,10 +145,10 @@ __device__ __forceinline__ int phuff(PReader &r, const ProgLds &L, const ProgTab
   const int w = (int)(r.buf >> 48);
   for (int l = 9; l <= 16; ++l) {
     const int code = w >> (16 - l);
-    if (code <= t.maxcode[l]) {
+    if (code <= (int)uni((uint32_t)t.maxcode[l])) {
       r.buf <<= l;
       r.bits -= l;
-      return t.vals[(t.valoff[l] + code) & 0xFF];
+      return (int)uni(t.vals[((int)uni((uint32_t)t.valoff[l]) + code) & 0xFF]);
     }
   }
   r.buf <<= 16; // corrupt data: libjpeg warns and returns symbol 0
@@ -166,10 +180,26 @@ __device__ __forceinline__ void prestart(PReader &r, const ProgLds &L) {
   }
 }
 
-// AC refinement correction bit on an already-nonzero coefficient.
-__device__ __forceinline__ void prefine(PReader &r, const ProgLds &L, int16_t &c, int p1, int m1) {
-  if (pget(r, L, 1) && (c & p1) == 0) c = (int16_t)(c >= 0 ? c + p1 : c + m1);
+// AC refinement correction bits for the already-nonzero positions in `seg`
+// (ascending zigzag order, one bit each, read 16 at a time): returns the
+// positions whose bit is 1. The corrections themselves (jdphuff.c: c += p1 or
+// m1 when (c & p1) == 0) are applied lane-parallel after the chunk.
+__device__ __forceinline__ uint64_t pcorr(PReader &r, const ProgLds &L, uint64_t seg) {
+  uint64_t res = 0;
+  while (seg) {
+    const int cnt = min(__popcll(seg), 16);
+    const int bits = pget(r, L, cnt);
+    for (int j = cnt - 1; j >= 0; --j) {
+      const uint64_t low = seg & (0ull - seg);
+      res |= ((bits >> j) & 1) ? low : 0ull;
+      seg ^= low;
+    }
+  }
+  return res;
 }
+
+__device__ __forceinline__ uint64_t mask_from(int k) { return k >= 64 ? 0ull : (~0ull << k); }
+__device__ __forceinline__ uint64_t mask_below(int k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
 
 // Stage scan bytes [base, min(base + kWin, lim)) into the window (all lanes).
 __device__ void load_window(ProgLds &L, const uint8_t *data, int64_t base, int64_t lim) {
@@ -193,14 +223,25 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
                                              int16_t *__restrict__ dcv,
                                              const int32_t *__restrict__ status) {
   __shared__ ProgLds L;
-  const int img = prog_img[blockIdx.x];
+  // chain 0: the DC scans (dcv only); chain 1 + c: component c's AC scans
+  // (coef slots 1..63 of its blocks). JPEG AC scans are single-component, so
+  // the chains touch disjoint data and run as independent workgroups; within
+  // a chain, scans keep file order (refinements follow their first scans).
+  // chain-major grid: consecutive workgroups are different images, so the
+  // long luma chains spread round-robin over all 8 XCDs; luma AC first
+  const int nimg = (int)(gridDim.x >> 2);
+  const int img = prog_img[blockIdx.x % nimg];
+  const int q = (int)(blockIdx.x / nimg);
+  const int chain = q == 0 ? 1 : (q == 1 ? 0 : q);
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
+  if (chain > d.ncomp) return;
   const int lane = threadIdx.x;
   const int64_t nblk = (int64_t)d.mcux * d.mcuy * d.bpm;
   // DC values start at zero: blocks no DC scan covers (the padding blocks of
   // non-interleaved DC scans) must not keep an earlier batch's value
-  for (int64_t b = lane; b < nblk; b += 64) dcv[d.coef_off + b] = 0;
+  if (chain == 0)
+    for (int64_t b = lane; b < nblk; b += 64) dcv[d.coef_off + b] = 0;
   int b0[3] = {0, 0, 0}, hmax = 1, vmax = 1;
   for (int c = 0; c < d.ncomp; ++c) {
     hmax = max(hmax, d.ch[c]);
@@ -215,6 +256,7 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
     const ProgScan &sc = scans[d.prog_first + si];
     const int ns = sc.ns, Ss = sc.ss, Se = sc.se, Ah = sc.ah, Al = sc.al;
     const bool dcband = Ss == 0;
+    if (dcband ? chain != 0 : chain != 1 + sc.comp[0]) continue; // another chain's scan
     __syncthreads();
     for (int k = 0; k < 4; ++k) {
       if (sc.tab[k] < 0) continue;
@@ -280,14 +322,27 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
         } else {
           const int4 *src = reinterpret_cast<const int4 *>(coef + gb * 64);
           int4 *dst = reinterpret_cast<int4 *>(L.blk[lane]);
+          uint64_t nz = 0;
 #pragma unroll
-          for (int q = 0; q < 8; ++q) dst[q] = src[q];
+          for (int q = 0; q < 8; ++q) {
+            const int4 v = src[q];
+            dst[q] = v;
+            const uint32_t w[4] = {(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              nz |= (uint64_t)((w[h] & 0xFFFFu) != 0) << (8 * q + 2 * h);
+              nz |= (uint64_t)((w[h] >> 16) != 0) << (8 * q + 2 * h + 1);
+            }
+          }
+          L.nzm[lane] = nz;
+          L.corr[lane] = 0;
         }
       }
       __syncthreads();
-      if (lane == 0) {
-        R.wb = L.win_base;
-        R.wl = L.win_lim;
+      const bool w0 = lane == 0; // the lane that stores
+      {
+        R.wb = (int64_t)uni64((uint64_t)L.win_base);
+        R.wl = (int64_t)uni64((uint64_t)L.win_lim);
         int slot = 0;
         for (int ui = 0; ui < nu; ++ui) {
           if (sc.restart) {
@@ -305,9 +360,9 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
               if (dcband && Ah == 0) { // decode_mcu_DC_first
                 const int t = phuff(R, L, L.tabs[i]);
                 pred[i] += pextend(pget(R, L, t), t);
-                L.dc[slot] = (int16_t)(pred[i] * (1 << Al));
+                if (w0) L.dc[slot] = (int16_t)(pred[i] * (1 << Al));
               } else if (dcband) { // decode_mcu_DC_refine
-                if (pget(R, L, 1)) L.dc[slot] = (int16_t)(L.dc[slot] | p1);
+                if (pget(R, L, 1) && w0) L.dc[slot] = (int16_t)(L.dc[slot] | p1);
               } else if (Ah == 0) { // decode_mcu_AC_first
                 if (eobrun > 0) {
                   --eobrun;
@@ -319,7 +374,8 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
                   const int r = rs >> 4, t = rs & 15;
                   if (t) {
                     k += r;
-                    blk[min(k, 63)] = (int16_t)(pextend(pget(R, L, t), t) * (1 << Al));
+                    const int v = pextend(pget(R, L, t), t) * (1 << Al);
+                    if (w0) blk[min(k, 63)] = (int16_t)v;
                   } else if (r == 15) {
                     k += 15;
                   } else {
@@ -329,13 +385,22 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
                     break;
                   }
                 }
-              } else { // decode_mcu_AC_refine
+              } else { // decode_mcu_AC_refine, on bit masks of the block
+                // jdphuff.c walks k one coefficient at a time: a nonzero
+                // (history) coefficient takes a correction bit, the (r+1)-th
+                // zero stops the walk and receives the new value. Here the
+                // history is the 64-bit mask nzh, the stop is found by
+                // clearing r zero bits, and the correction bits of the
+                // nonzeros passed are read in bulk (pcorr).
                 int16_t *blk = L.blk[slot];
+                const uint64_t nzh = uni64(L.nzm[slot]);
+                const uint64_t band = mask_below(Se + 1);
+                uint64_t corr = 0;
                 int k = Ss;
                 if (eobrun == 0) {
                   for (; k <= Se; ++k) {
                     const int rs = phuff(R, L, L.tabs[0]);
-                    int r = rs >> 4;
+                    const int r = rs >> 4;
                     const int t = rs & 15;
                     int sv = 0;
                     if (t) {
@@ -345,31 +410,36 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
                       if (r) eobrun += pget(R, L, r);
                       break;
                     }
-                    do {
-                      int16_t &c = blk[min(k, 63)];
-                      if (c != 0) prefine(R, L, c, p1, m1);
-                      else if (--r < 0) break;
-                      ++k;
-                    } while (k <= Se);
-                    if (sv) blk[min(k, 63)] = (int16_t)sv;
+                    uint64_t z = ~nzh & mask_from(k) & band;
+                    for (int q = 0; q < r && z; ++q) z &= z - 1;
+                    const int stop = z ? __ffsll((unsigned long long)z) - 1 : Se + 1;
+                    corr |= pcorr(R, L, nzh & mask_from(k) & mask_below(stop));
+                    k = stop;
+                    if (sv && w0) blk[min(k, 63)] = (int16_t)sv;
                   }
                 }
                 if (eobrun > 0) {
-                  for (; k <= Se; ++k) {
-                    int16_t &c = blk[k];
-                    if (c != 0) prefine(R, L, c, p1, m1);
-                  }
+                  corr |= pcorr(R, L, nzh & mask_from(k) & band);
                   --eobrun;
                 }
+                if (w0) L.corr[slot] = corr;
               }
             }
           }
         }
-        L.pos = R.pos;
+        if (w0) L.pos = R.pos;
       }
       __syncthreads();
       if (lane < nbk) {
         const int64_t gb = L.bidx[lane];
+        if (!dcband && Ah != 0) { // apply this block's refinement corrections
+          int16_t *blk = L.blk[lane];
+          for (uint64_t cm = L.corr[lane]; cm; cm &= cm - 1) {
+            const int pos = __ffsll((unsigned long long)cm) - 1;
+            const int c = blk[pos];
+            if ((c & p1) == 0) blk[pos] = (int16_t)(c >= 0 ? c + p1 : c + m1);
+          }
+        }
         if (dcband) {
           dcv[gb] = L.dc[lane];
         } else {
@@ -392,7 +462,7 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
 
 hipError_t launch_prog(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_prog == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prog, dim3(p.n_prog), dim3(64), 0, s, p.descs, p.prog_img, p.pscans, p.ptabs,
+  hipLaunchKernelGGL(k_prog, dim3(4 * p.n_prog), dim3(64), 0, s, p.descs, p.prog_img, p.pscans, p.ptabs,
                      w.data, w.coef, w.dcv, w.status);
   return hipGetLastError();
 }
