@@ -37,8 +37,18 @@ def run(rank, world, port, outdir):
     b = ShardedBatchSampler(rank, world, compute=oracle.sharded_batch_ranges)
     rng = b.ranges(sum(FOOD101_FRAGMENTS), 128)
     m = agree_max(rank * 10 + 3)
+    # map-style DistributedSampler: num_replicas/rank from the process group,
+    # as lance_map_style.py:58 constructs it (oracle standing in for the kernel)
+    from ldt_amd import DistributedSampler
+
+    def dist_compute(n, W, r, shuffle, seed, drop_last):
+        return oracle.distributed_indices(n, W, r, shuffle, seed, 0, drop_last)
+
+    ds = DistributedSampler(range(1001), seed=7, compute=dist_compute)
+    ds.set_epoch(2)
+    didx = list(ds)
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
         json.dump({"padded": len(recs), "unpadded": len(recs_nopad), "ranges": rng, "max": m,
-                   "calls": calls}, f)
+                   "calls": calls, "dist_idx": didx, "dist_rank": ds.rank, "dist_world": ds.num_replicas}, f)
     dist.barrier()
     dist.destroy_process_group()

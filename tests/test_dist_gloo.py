@@ -32,3 +32,14 @@ def test_fragment_pad_consensus_world2(tmp_path):
     assert r0["calls"][:2] == [-1, 300] and r1["calls"][:2] == [-1, 300]
     rows = sorted(tuple(x) for x in r0["ranges"] + r1["ranges"])
     assert rows[0][0] == 0 and rows[-1][1] == 75750 and len(rows) == 592
+    # DistributedSampler: rank/world from the group; the two ranks together
+    # cover every index (1001 rows padded to 1002: one repeat), as torch's
+    assert (r0["dist_rank"], r1["dist_rank"], r0["dist_world"]) == (0, 1, 2)
+    assert len(r0["dist_idx"]) == len(r1["dist_idx"]) == 501
+    assert sorted(set(r0["dist_idx"]) | set(r1["dist_idx"])) == list(range(1001))
+    from torch.utils.data import DistributedSampler as TorchDS
+
+    for r, got in ((0, r0["dist_idx"]), (1, r1["dist_idx"])):
+        t = TorchDS(range(1001), num_replicas=2, rank=r, seed=7)
+        t.set_epoch(2)
+        assert got == list(t)
