@@ -30,8 +30,9 @@ namespace ldt {
 
 namespace {
 
-constexpr int kWin = 16384; // scan bytes staged in LDS
-constexpr int kChunk = 64;  // blocks staged per round (one per lane)
+constexpr int kWin = 4096;  // scan bytes staged in LDS (per wave)
+constexpr int kChunk = 32;  // blocks staged per round (one per lane)
+constexpr int kWaves = 4;   // scans of one chain in flight (one wave each)
 
 struct ProgLds {
   union {
@@ -203,7 +204,7 @@ __device__ __forceinline__ uint64_t mask_below(int k) { return k >= 64 ? ~0ull :
 
 // Stage scan bytes [base, min(base + kWin, lim)) into the window (all lanes).
 __device__ void load_window(ProgLds &L, const uint8_t *data, int64_t base, int64_t lim) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int64_t n = min((int64_t)kWin, lim - base);
   for (int64_t o = lane; o < n; o += 64) L.win[o] = data[base + o];
   if (lane == 0) {
@@ -212,9 +213,16 @@ __device__ void load_window(ProgLds &L, const uint8_t *data, int64_t base, int64
   }
 }
 
+// Orders a wave's LDS accesses across lanes (the wave's LDS operations
+// execute in order; this keeps the compiler from moving them across).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 } // namespace
 
-__global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
+__global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict__ descs,
                                              const int32_t *__restrict__ prog_img,
                                              const ProgScan *__restrict__ scans,
                                              const ProgTab *__restrict__ ptabs,
@@ -222,7 +230,8 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
                                              int16_t *__restrict__ coef,
                                              int16_t *__restrict__ dcv,
                                              const int32_t *__restrict__ status) {
-  __shared__ ProgLds L;
+  __shared__ ProgLds Lw[kWaves];
+  __shared__ int progress[kMaxProgScans]; // chunks of each chain scan written back
   // chain 0: the DC scans (dcv only); chain 1 + c: component c's AC scans
   // (coef slots 1..63 of its blocks). JPEG AC scans are single-component, so
   // the chains touch disjoint data and run as independent workgroups; within
@@ -236,7 +245,16 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   if (chain > d.ncomp) return;
-  const int lane = threadIdx.x;
+  for (int i = threadIdx.x; i < kMaxProgScans; i += 64 * kWaves) progress[i] = 0;
+  __syncthreads(); // the only workgroup barrier: waves run independently from here
+  // AC chains are pipelined: the chain's j-th scan runs on wave j % kWaves and
+  // processes its chunk c once scan j-1 has written chunk c back (all AC scans
+  // of a component walk the same block order in the same chunks). The DC chain
+  // (interleaved and per-component DC scans chunk differently) runs on wave 0.
+  const int wave = (int)(threadIdx.x >> 6);
+  const int lane = (int)(threadIdx.x & 63);
+  if (chain == 0 && wave != 0) return;
+  ProgLds &L = Lw[wave];
   const int64_t nblk = (int64_t)d.mcux * d.mcuy * d.bpm;
   // DC values start at zero: blocks no DC scan covers (the padding blocks of
   // non-interleaved DC scans) must not keep an earlier batch's value
@@ -252,12 +270,17 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
   PReader R;
   R.data = data;
   int pred[4] = {0, 0, 0, 0};
+  int jc = -1; // index of the scan within the chain
   for (int si = 0; si < d.prog_count; ++si) {
     const ProgScan &sc = scans[d.prog_first + si];
     const int ns = sc.ns, Ss = sc.ss, Se = sc.se, Ah = sc.ah, Al = sc.al;
     const bool dcband = Ss == 0;
     if (dcband ? chain != 0 : chain != 1 + sc.comp[0]) continue; // another chain's scan
-    __syncthreads();
+    ++jc;
+    const bool piped = chain != 0;
+    if (piped && jc % kWaves != wave) continue; // another wave's scan
+    const bool wait_prev = piped && jc > 0;
+    wave_sync();
     for (int k = 0; k < 4; ++k) {
       if (sc.tab[k] < 0) continue;
       const uint32_t *src = reinterpret_cast<const uint32_t *>(ptabs + sc.tab[k]);
@@ -266,7 +289,7 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
     }
     const int64_t lim = sc.data_off + sc.data_len + 2; // through the ending marker
     load_window(L, data, sc.data_off, lim);
-    __syncthreads();
+    wave_sync();
     // units: MCUs of the interleaved grid, or the component's own blocks
     int ux, uy, bpu = 0;
     if (ns == 1) {
@@ -294,9 +317,12 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
     int64_t eobrun = 0;
     int togo = sc.restart;
     const int p1 = 1 << Al, m1 = -(1 << Al);
-    for (int64_t u0 = 0; u0 < units; u0 += upc) {
+    for (int64_t u0 = 0, ci = 0; u0 < units; u0 += upc, ++ci) {
       const int nu = (int)min((int64_t)upc, units - u0);
       const int nbk = nu * bpu;
+      if (wait_prev) // scan jc-1 has written this chunk back
+        while (__hip_atomic_load(&progress[jc - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= ci)
+          __builtin_amdgcn_s_sleep(1);
       // stage the chunk's blocks: lane j -> block j of the chunk, scan order
       if (lane < nbk) {
         const int64_t u = u0 + lane / bpu;
@@ -338,7 +364,7 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
           L.corr[lane] = 0;
         }
       }
-      __syncthreads();
+      wave_sync();
       const bool w0 = lane == 0; // the lane that stores
       {
         R.wb = (int64_t)uni64((uint64_t)L.win_base);
@@ -429,7 +455,7 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
         }
         if (w0) L.pos = R.pos;
       }
-      __syncthreads();
+      wave_sync();
       if (lane < nbk) {
         const int64_t gb = L.bidx[lane];
         if (!dcband && Ah != 0) { // apply this block's refinement corrections
@@ -449,20 +475,26 @@ __global__ void __launch_bounds__(64) k_prog(const ImgDesc *__restrict__ descs,
           for (int q = 0; q < 8; ++q) dst[q] = src[q];
         }
       }
+      if (piped) { // publish chunk ci once the wave's stores are done
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0)
+          __hip_atomic_store(&progress[jc], (int)(ci + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       // keep at least half a window of bytes ahead of the reader
+      wave_sync();
       const int64_t pos = L.pos;
       if (pos - L.win_base > kWin / 2 && L.win_lim < lim) {
-        __syncthreads();
+        wave_sync();
         load_window(L, data, pos, lim);
       }
-      __syncthreads();
+      wave_sync();
     }
   }
 }
 
 hipError_t launch_prog(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_prog == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prog, dim3(4 * p.n_prog), dim3(64), 0, s, p.descs, p.prog_img, p.pscans, p.ptabs,
+  hipLaunchKernelGGL(k_prog, dim3(4 * p.n_prog), dim3(64 * kWaves), 0, s, p.descs, p.prog_img, p.pscans, p.ptabs,
                      w.data, w.coef, w.dcv, w.status);
   return hipGetLastError();
 }
