@@ -122,10 +122,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # LDT_BENCH_BACKEND=gloo: rehearsal of the multi-rank path on a 1-GPU box
+    # (ranks then share the devices round-robin); the real runs use RCCL
+    backend = os.environ.get("LDT_BENCH_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        torch.cuda.set_device(local % torch.cuda.device_count() if backend != "nccl" else local)
+        dist.init_process_group(backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -203,7 +206,7 @@ def main():
     stages = prof.stage_times(reset=True)
     if args.workload != "c5":
         pipe.check()  # every decoded image status OK
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
