@@ -16,7 +16,7 @@ for w in c2 c1 c4 c5 c2p; do
   echo "$w: $(head -c 200 $O/bench_$w.json)"
 done
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_c2.log 2>&1 || { tail -5 $O/prof_c2.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $O/prof_c2.log 2>&1 || { tail -5 $O/prof_c2.log; exit 1; }
 for w in c2 c5; do
   bash $R/tools/traffic.sh $w ${T}_$w > /dev/null || exit 1
   cp $R/gpurun_out/traffic_${T}_$w/summary.json $O/traffic_$w.json
