@@ -142,12 +142,27 @@ class ArrowDataset:
         return pa.Table.from_batches(parts).combine_chunks().to_batches()[0]
 
     def take(self, indices: Sequence[int], columns=None) -> pa.Table:
+        """Rows at `indices` (dataset order), in the given order: one vectorised
+        Table.take per fragment touched, then the original order restored."""
         idx = np.asarray(indices, dtype=np.int64)
-        out = []
-        for i in idx:
-            f = int(np.searchsorted(self._starts, i, side="right") - 1)
-            out.append(self._frags[f].read_slice(int(i - self._starts[f]), int(i - self._starts[f] + 1), columns))
-        return pa.Table.from_batches(out) if out else self.schema.empty_table()
+        if idx.size == 0:
+            t = self.schema.empty_table()
+            return t.select(columns) if columns is not None else t
+        if idx.min() < 0 or idx.max() >= self.count_rows():
+            raise IndexError("row index out of range")
+        frag = np.searchsorted(self._starts, idx, side="right") - 1
+        parts, pos = [], []
+        for fid in np.unique(frag):
+            sel = np.nonzero(frag == fid)[0]
+            t = self._frags[int(fid)]._tbl()
+            if columns is not None:
+                t = t.select(columns)
+            parts.append(t.take(pa.array(idx[sel] - self._starts[fid])))
+            pos.append(sel)
+        tbl = pa.concat_tables(parts) if len(parts) > 1 else parts[0]
+        if len(parts) > 1:
+            tbl = tbl.take(pa.array(np.argsort(np.concatenate(pos), kind="stable")))
+        return tbl
 
 
 def dataset(uri: str) -> ArrowDataset:
@@ -208,19 +223,80 @@ class SafeLanceDataset(Dataset):
         return self._d().take(list(indices), self.columns).to_pylist()
 
 
-def _passthrough(rows):
-    return rows
+def _pack_rows(rows):
+    """Worker side: the batch as torch tensors over the Arrow buffers (image
+    bytes, int32 offsets, labels), so DataLoader moves them through shared
+    memory instead of pickling megabytes through its result pipe."""
+    if not isinstance(rows, pa.RecordBatch):  # _ArrowRows fetched it packed already
+        from .transforms import pack_rows
+
+        rows = pack_rows(rows)
+    img = rows.column(rows.schema.get_field_index("image"))
+    if pa.types.is_large_binary(img.type):
+        img = img.cast(pa.binary())
+    off = np.frombuffer(img.buffers()[1], np.int32, len(img) + 1, img.offset * 4)
+    data = np.frombuffer(img.buffers()[2], np.uint8) if img.buffers()[2] is not None else np.zeros(0, np.uint8)
+    out = {"offsets": torch.from_numpy(off - off[0]),
+           "data": torch.from_numpy(data[off[0]:off[-1]].copy())}
+    if img.null_count:
+        out["valid"] = torch.from_numpy(np.asarray(img.is_valid()))
+    if "label" in rows.schema.names:
+        out["label"] = torch.from_numpy(rows.column(rows.schema.get_field_index("label")).to_numpy(zero_copy_only=False).astype(np.int64))
+    return out
+
+
+def _unpack_rows(packed) -> pa.RecordBatch:
+    """Main-process side of _pack_rows: an Arrow RecordBatch over the shared
+    tensors' memory (no copy)."""
+    n = packed["offsets"].numel() - 1
+    valid = None
+    if "valid" in packed:
+        valid = pa.array(packed["valid"].numpy()).buffers()[1]
+    img = pa.Array.from_buffers(pa.binary(), n, [valid, pa.py_buffer(packed["offsets"].numpy()),
+                                                  pa.py_buffer(packed["data"].numpy())])
+    cols, names = [img], ["image"]
+    if "label" in packed:
+        cols.append(pa.array(packed["label"].numpy()))
+        names.append("label")
+    return pa.RecordBatch.from_arrays(cols, names=names)
+
+
+class _ArrowRows(Dataset):
+    """SafeLanceDataset seen by get_safe_loader's workers when the collate runs
+    on the GPU: a batch of indices becomes one Arrow ``take`` (no per-row
+    Python dicts, which the GPU collate would only pack back into Arrow)."""
+
+    def __init__(self, ds: "SafeLanceDataset"):
+        self.ds = ds
+
+    def __len__(self) -> int:
+        return len(self.ds)
+
+    def __getitem__(self, i: int):
+        return self.ds[i]
+
+    def __getitems__(self, indices):
+        t = self.ds._d().take(list(indices), self.ds.columns).combine_chunks()
+        b = t.to_batches()
+        return b[0] if b else pa.RecordBatch.from_pylist([], schema=t.schema)
 
 
 class _DeviceCollateLoader:
-    """DataLoader whose workers fetch rows; collate runs in the main process."""
+    """DataLoader whose workers fetch rows and pack them into one Arrow
+    RecordBatch per batch; the GPU collate runs in the main process (with
+    ``make_collate_fn(prefetch=k)``: k batches ahead on side streams)."""
 
     def __init__(self, loader: DataLoader, collate_fn):
         self.loader, self.collate_fn = loader, collate_fn
 
     def __iter__(self):
-        for rows in self.loader:
-            yield self.collate_fn(rows)
+        pre = getattr(self.collate_fn, "_ldt_prefetch_iter", None)
+        batches = (_unpack_rows(p) for p in self.loader)
+        if pre is not None:
+            yield from pre(batches)
+            return
+        for rb in batches:
+            yield self.collate_fn(rb)
 
     def __len__(self):
         return len(self.loader)
@@ -231,8 +307,10 @@ def get_safe_loader(dataset, batch_size: int, sampler=None, shuffle: bool = Fals
     """``lance.torch.data.get_safe_loader`` stand-in (lance_map_style.py:60-69)."""
     device_collate = getattr(collate_fn, "_ldt_device_collate", False)
     mp_ctx = kwargs.pop("multiprocessing_context", "spawn" if num_workers > 0 else None)
+    if device_collate and isinstance(dataset, SafeLanceDataset):
+        dataset = _ArrowRows(dataset)
     dl = DataLoader(dataset, batch_size=batch_size, sampler=sampler, shuffle=shuffle if sampler is None else False,
-                    num_workers=num_workers, collate_fn=_passthrough if device_collate else collate_fn,
+                    num_workers=num_workers, collate_fn=_pack_rows if device_collate else collate_fn,
                     pin_memory=False if device_collate else pin_memory,
                     persistent_workers=persistent_workers if num_workers > 0 else False,
                     multiprocessing_context=mp_ctx, **kwargs)

@@ -186,7 +186,10 @@ def collate_fn(batch_of_dicts, *, device=None, normalize=None):
     """collate_fn: list of ``{"image": bytes, "label": int}`` -> stacked tensors
     (lance_map_style.py:21-44). The bytes are packed into one Arrow buffer
     (zero-copy of the Python ``bytes`` objects is impossible; this is the one
-    host copy) and decoded on the GPU."""
+    host copy) and decoded on the GPU. get_safe_loader's workers may hand over
+    the rows already packed as a ``pa.RecordBatch`` (``pack_rows``)."""
+    if isinstance(batch_of_dicts, pa.RecordBatch):
+        return decode_tensor_image(batch_of_dicts, device=device, normalize=normalize)
     images = [item["image"] for item in batch_of_dicts]
     labels = [item["label"] for item in batch_of_dicts]
     arr = pa.array(images, type=pa.binary())
@@ -194,14 +197,40 @@ def collate_fn(batch_of_dicts, *, device=None, normalize=None):
     return {"image": img, "label": lbl}
 
 
+def pack_rows(batch_of_dicts) -> pa.RecordBatch:
+    """DataLoader-worker side of the GPU collate: the rows' bytes and labels
+    as one Arrow RecordBatch (pickled as a few buffers instead of one Python
+    object per row)."""
+    cols = [pa.array([item["image"] for item in batch_of_dicts], type=pa.binary())]
+    names = ["image"]
+    if batch_of_dicts and "label" in batch_of_dicts[0]:
+        cols.append(pa.array([item["label"] for item in batch_of_dicts], type=pa.int64()))
+        names.append("label")
+    return pa.RecordBatch.from_arrays(cols, names=names)
+
+
 collate_fn._ldt_device_collate = True  # get_safe_loader: decode in the main process
 
 
-def make_collate_fn(device=None, normalize=None):
-    """A collate_fn bound to a device / Normalize setting."""
+def make_collate_fn(device=None, normalize=None, prefetch: int = 0, depth: int = 3):
+    """A collate_fn bound to a device / Normalize setting.
+
+    ``prefetch=k`` (k < depth): ``get_safe_loader`` then decodes k batches ahead
+    on a ``DecodePipeline`` (the workers' next batches decode while the consumer
+    uses the current one); per-image errors surface asynchronously, as with
+    ``make_to_tensor_fn(prefetch=k)``."""
     def _fn(batch_of_dicts):
         return collate_fn(batch_of_dicts, device=device, normalize=normalize)
     _fn._ldt_device_collate = True
+    if prefetch > 0:
+        state = {}
+
+        def _iterate(record_batches):
+            if "pipe" not in state:
+                state["pipe"] = DecodePipeline(depth=depth, device=device)
+            return state["pipe"].prefetch(record_batches, ahead=min(prefetch, depth - 1), normalize=normalize)
+
+        _fn._ldt_prefetch_iter = _iterate
     return _fn
 
 
