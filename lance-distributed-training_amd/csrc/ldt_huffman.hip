@@ -273,6 +273,9 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
   while (go) {
     const bool dc = st.k == 0;
     cursor += dc ? 1 : 0;
+    // corrupt streams can count more blocks than the segment has, so a range
+    // may enter mid-block with its cursor outside [0, total): no stores then
+    const bool inb = (uint32_t)cursor < (uint32_t)total;
     const uint32_t pk = R.peek();
     const uint32_t e = lookup(dec, st, pk);
     const int v = ext_value(pk, e);
@@ -284,11 +287,11 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     if (dc) dcv_seg[cursor] = (int16_t)v;
     const bool direct = nz && first && g == shared_g;
 #ifndef LDT_EXP_NOSTORE
-    if (direct) blk[slot] = (int16_t)v;
+    if (direct && inb) blk[slot] = (int16_t)v;
 #endif
     const bool buf = nz && !direct;
     const bool newg = buf && g != grp;
-    if (newg && grp >= 0) store_group(blk + 8 * grp, lo, hi);
+    if (newg && grp >= 0 && inb) store_group(blk + 8 * grp, lo, hi);
     lo = newg ? 0ull : lo;
     hi = newg ? 0ull : hi;
     grp = newg ? g : grp;
@@ -297,13 +300,13 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     hi |= (slot & 4) ? x : 0ull;
     R.consume((int)(e & 31));
     const bool end = st.k + adv >= 64;
-    if (end && grp >= 0) store_group(blk + 8 * grp, lo, hi);
+    if (end && grp >= 0 && inb) store_group(blk + 8 * grp, lo, hi);
     grp = end ? -1 : grp;
     first = first && !end;
     advance(st, dec, adv);
     go = R.p < stop && !(st.k == 0 && cursor + 1 >= total);
   }
-  if (grp >= 0) { // the open block continues in the next range
+  if (grp >= 0 && (uint32_t)cursor < (uint32_t)total) { // the open block continues in the next range
     int16_t *p = coef_seg + (int64_t)cursor * 64 + 8 * grp;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {

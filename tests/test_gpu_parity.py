@@ -550,3 +550,63 @@ def test_map_style_loader_prefetch_matches_sync(tmp_path):
     assert np.array_equal(outs[1][0]["image"][0].cpu().numpy(), oracle.jpeg_to_tensor(cells[first]))
     assert int(outs[1][0]["label"][0]) == int(labels[first])
     del order
+
+
+def _sos_end(b: bytes) -> int:
+    """Offset of the first entropy-coded byte (after the first SOS header)."""
+    i = 2
+    while i + 4 <= len(b):
+        m, L = b[i + 1], (b[i + 2] << 8) | b[i + 3]
+        if m == 0xDA:
+            return i + 2 + L
+        i += 2 + L
+    raise ValueError("no SOS")
+
+
+@pytest.mark.parametrize("kind", ["c2", "c4", "prog"])
+def test_corrupt_entropy_data_is_contained(kind):
+    """Robustness: random bit flips, byte overwrites and stray markers in the
+    entropy-coded data. A batch holding a corrupt image next to a valid one
+    must not fault the GPU; the valid image stays bit-exact whether or not the
+    corrupt one is reported (libjpeg decodes some corrupt streams to garbage
+    with a warning; this build decodes them too or reports LDT_IMG_CORRUPT),
+    and a clean batch afterwards is bit-exact (the all-zero coefficient
+    invariant is restored)."""
+    import ldt_amd
+    from ldt_amd import synth
+
+    if kind == "c2":
+        base = synth.encode(synth.field(512, 512, 5, 6.0), quality=90)
+    elif kind == "c4":
+        base = synth.encode(synth.field(375, 500, 6, 6.0), quality=90, restart_marker_rows=1)
+    else:
+        base = synth.encode(synth.field(256, 320, 7, 6.0), quality=85, progressive=True)
+    good = synth.encode(synth.field(300, 200, 8, 6.0))
+    exp_good = oracle.jpeg_to_tensor(good)
+    rng = np.random.default_rng({"c2": 1, "c4": 2, "prog": 3}[kind])
+    s0 = _sos_end(base)
+    for trial in range(24):
+        b = bytearray(base)
+        mode = trial % 4
+        for _ in range(int(rng.integers(1, 8))):
+            p = int(rng.integers(s0, len(b) - 2))
+            if mode == 0:
+                b[p] ^= 1 << int(rng.integers(0, 8))
+            elif mode == 1:
+                b[p] = int(rng.integers(0, 256))
+            elif mode == 2:
+                b[p:p + 2] = bytes([0xFF, int(rng.choice([0x00, 0xD0, 0xD3, 0xD9, 0xC4, 0xFF]))])
+            else:
+                del b[p:p + int(rng.integers(1, 64))]
+        cells = [good, bytes(b), good]
+        try:
+            out = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+            got = [out[0], out[2]]
+        except ldt_amd.ImageDecodeError as e:
+            assert set(e.rows) == {1}, (kind, trial, e.rows)
+            continue
+        for g in got:
+            _check(g, exp_good, f"{kind} trial {trial}: valid neighbour")
+    img = ldt_amd.decode_tensor_image(_batch([base, good]))["image"].cpu().numpy()
+    _check(img[0], oracle.jpeg_to_tensor(base), f"{kind}: clean batch after corrupt ones")
+    _check(img[1], exp_good, f"{kind}: clean batch after corrupt ones")
