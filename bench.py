@@ -179,8 +179,6 @@ def main():
                 c.set_option(_lib.OPT_SYNC_WARM, int(os.environ["LDT_SYNC_WARM"]))
             if os.environ.get("LDT_SUBSEQ_FIT"):
                 c.set_option(_lib.OPT_SUBSEQ_FIT, int(os.environ["LDT_SUBSEQ_FIT"]))
-            if os.environ.get("LDT_DEBUG_SKIP"):  # marginal-cost experiments only (wrong outputs)
-                c.set_option(_lib.OPT_DEBUG_SKIP, int(os.environ["LDT_DEBUG_SKIP"]))
 
         def step():
             b = batches[it[0] % nb]

@@ -63,15 +63,13 @@ extern "C" {
 #define LDT_OPT_PROFILE 4     /* 1: record HIP events around every stage on the
                                  caller's stream (read with ldt_stage_times)    */
 #define LDT_OPT_RESIZE_IMPL 5 /* 0 auto (default): one wave per band; 2: the
-                                 banded workgroup kernel (cross-check)          */
+                                 streaming workgroup kernel that serves sources
+                                 wider than 1120 px (cross-check)               */
 #define LDT_OPT_SUBSEQ_FIT 6  /* 1 (default): per image, shrink the subsequence
                                  length so its slots fill whole workgroups;
                                  0: every image uses LDT_OPT_SUBSEQ_BITS        */
 #define LDT_OPT_SYNC_WARM 7   /* parallel decoder phase 1 starts this % of S
                                  before each range (0..200, default 0)         */
-#define LDT_OPT_DEBUG_SKIP 8  /* measurement only: bit 0 skips the resize
-                                 launch, bit 1 the IDCT launch (outputs are
-                                 then WRONG; marginal-cost experiments)         */
 
 /* ---- stages reported by ldt_stage_times ---- */
 #define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */

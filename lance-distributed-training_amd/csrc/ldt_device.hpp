@@ -39,6 +39,31 @@ __device__ __forceinline__ int block_excl_scan256(int v, int *scratch, int *tota
   return base + inc - v;
 }
 
+// 64-bit variant (row and batch totals of large datasets pass 2^31).
+// `scratch` must hold >= 4 int64; contains a __syncthreads.
+__device__ __forceinline__ int64_t block_excl_scan256_i64(int64_t v, long long *scratch,
+                                                          int64_t *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) scratch[wave] = inc;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int64_t s = scratch[w];
+    if (w < wave) base += s;
+    tot += s;
+  }
+  *total = tot;
+  __syncthreads();
+  return base + inc - v;
+}
+
 // ---------------------------------------------------------------------------
 // Pillow Resample.c precompute_coeffs + normalize_coeffs_8bpc for one output
 // index, BILINEAR (support 1.0), box (0, in). IEEE double, no contraction, so

@@ -245,10 +245,6 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
 // it or the block ends. Groups a neighbouring range may also write (a block
 // straddling the range boundary) are written slot by slot.
 __device__ __forceinline__ void store_group(int16_t *__restrict__ p, uint64_t lo, uint64_t hi) {
-#ifdef LDT_EXP_NOSTORE // experiment build: time the decode without coefficient stores
-  if (lo == 0x0123456789abcdefull) *reinterpret_cast<uint4 *>(p) = make_uint4(0, 0, 0, 0);
-  return;
-#endif
   *reinterpret_cast<uint4 *>(p) =
       make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
@@ -286,9 +282,7 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     int16_t *__restrict__ blk = coef_seg + (int64_t)cursor * 64;
     if (dc) dcv_seg[cursor] = (int16_t)v;
     const bool direct = nz && first && g == shared_g;
-#ifndef LDT_EXP_NOSTORE
     if (direct && inb) blk[slot] = (int16_t)v;
-#endif
     const bool buf = nz && !direct;
     const bool newg = buf && g != grp;
     if (newg && grp >= 0 && inb) store_group(blk + 8 * grp, lo, hi);

@@ -7,8 +7,8 @@
 //   k_huff_*      baseline Huffman decode of each segment into int16 DCT
 //                 coefficients, natural order, MCU-major block layout
 //                 (jdhuff.c decode_mcu restated; see ldt_huffman.hip).
-//   k_idct        dequantise + JDCT_ISLOW 8x8 IDCT (jidctint.c), 8 lanes per
-//                 block, column/row passes staged through LDS, uint8 planes.
+//   k_idct        dequantise + JDCT_ISLOW 8x8 IDCT (jidctint.c), one lane per
+//                 block (both passes in registers), uint8 planes.
 //   k_resize<S>   fused chroma fancy-upsampling (jdsample.c) + YCbCr->RGB
 //                 (jdcolor.c) + Pillow BILINEAR Resize((224,224)) (Resample.c,
 //                 22-bit fixed point, horizontal-then-vertical, uint8
@@ -330,9 +330,7 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
 }
 
 // ---------------------------------------------------------------------------
-// k_idct: jidctint.c jpeg_idct_islow. 8 lanes per block (lane = row/column),
-// 32 blocks per 256-thread workgroup. LDS stride 72 dwords per block keeps
-// the column pass conflict-free.
+// k_idct: jidctint.c jpeg_idct_islow, one lane per 8x8 block (see below).
 // ---------------------------------------------------------------------------
 #define FIX_0_298631336 2446
 #define FIX_0_390180644 3196
@@ -542,6 +540,28 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
   }
 }
 
+// Rows whose decode failed: the resize kernels skip them, so their outputs
+// are set here to defined values — zeros for the image and -100 for the label
+// (torch.nn.CrossEntropyLoss's default ignore_index) — in case an
+// asynchronous consumer (prefetching iterators) uses the batch before the
+// per-row status is read. One workgroup per row; rows that decoded return.
+__global__ void __launch_bounds__(256) k_fill_failed(const int32_t *__restrict__ status,
+                                                     float *__restrict__ out,
+                                                     int64_t *__restrict__ out_labels) {
+  const int img = blockIdx.x;
+  if (status[img] == 0) return;
+  float4 *o = reinterpret_cast<float4 *>(out + (int64_t)img * 3 * kOut * kOut);
+  for (int i = threadIdx.x; i < 3 * kOut * kOut / 4; i += 256) o[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (threadIdx.x == 0 && out_labels != nullptr) out_labels[img] = -100;
+}
+
+hipError_t launch_fill_failed(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
+                              hipStream_t s) {
+  if (p.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_failed, dim3(p.n), dim3(256), 0, s, w.status, out, out_labels);
+  return hipGetLastError();
+}
+
 // Test hook: coefficient tables for one (in, out) pair.
 __global__ void k_resample_coeffs(int inSize, int outSize, int ksize, int32_t *bounds,
                                   int32_t *kk) {
@@ -724,42 +744,40 @@ __global__ void __launch_bounds__(256) k_shard_fragments(const int64_t *frag_row
                                                          int64_t pad_to, int64_t *out,
                                                          int64_t capacity, int64_t *count,
                                                          int64_t *local_count) {
-  __shared__ int sh_scan[8];
+  __shared__ long long sh_scan[8];
   __shared__ long long sh_tot[3]; // own batches, global batches, rows
   const int tid = threadIdx.x;
   if (tid == 0) {
     sh_tot[0] = sh_tot[1] = sh_tot[2] = 0;
   }
   __syncthreads();
-  // pass 1: own records
+  // pass 1: own records (64-bit scans: a dataset may hold 2^31 rows or more)
   for (int f0 = 0; f0 < nfrag; f0 += 256) {
     const int f = f0 + tid;
-    int64_t rows = f < nfrag ? frag_rows[f] : 0;
-    int64_t nbf = (rows + bsz - 1) / bsz;
-    int own = (f < nfrag && (f % world) == rank) ? (int)nbf : 0;
-    int tot_own, tot_all, tot_rows_i;
-    int own_ex = block_excl_scan256(own, sh_scan, &tot_own);
-    int all_ex = block_excl_scan256((int)nbf, sh_scan, &tot_all);
-    int row_ex = block_excl_scan256((int)rows, sh_scan, &tot_rows_i);
+    const int64_t rows = f < nfrag ? frag_rows[f] : 0;
+    const int64_t nbf = (rows + bsz - 1) / bsz;
+    const int64_t own = (f < nfrag && (f % world) == rank) ? nbf : 0;
+    int64_t tot_own, tot_all, tot_rows;
+    const int64_t own_ex = block_excl_scan256_i64(own, sh_scan, &tot_own);
+    (void)block_excl_scan256_i64(nbf, sh_scan, &tot_all);
+    const int64_t row_ex = block_excl_scan256_i64(rows, sh_scan, &tot_rows);
     const int64_t own_base = sh_tot[0] + own_ex;
     const int64_t gstart = sh_tot[2] + row_ex;
-    for (int j = 0; j < own; ++j) {
+    for (int64_t j = 0; j < own; ++j) {
       const int64_t idx = own_base + j;
-      if (idx < capacity) {
-        int64_t *rec = out + idx * 5;
-        rec[0] = f;
-        rec[1] = (int64_t)j * bsz;
-        rec[2] = min((int64_t)(j + 1) * bsz, rows);
-        rec[3] = gstart + (int64_t)j * bsz;
-        rec[4] = 0;
-      }
+      if (idx >= capacity) break;
+      int64_t *rec = out + idx * 5;
+      rec[0] = f;
+      rec[1] = j * bsz;
+      rec[2] = min((j + 1) * bsz, rows);
+      rec[3] = gstart + j * bsz;
+      rec[4] = 0;
     }
-    (void)all_ex;
     __syncthreads();
     if (tid == 0) {
       sh_tot[0] += tot_own;
       sh_tot[1] += tot_all;
-      sh_tot[2] += tot_rows_i;
+      sh_tot[2] += tot_rows;
     }
     __syncthreads();
   }

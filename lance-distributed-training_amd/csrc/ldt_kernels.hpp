@@ -67,16 +67,14 @@ hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s);
 // Progressive (SOF2) images: serial per-scan decode into coef/dcv (ldt_prog.hip).
 hipError_t launch_prog(const DevPlan &p, const DevWork &w, hipStream_t s);
+// Failed rows: zero image, label -100 (after the resize kernels).
+hipError_t launch_fill_failed(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
+                              hipStream_t s);
 hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
                               hipStream_t s);
-// Banded resize (ldt_resize.hip). Return false when the geometry does not fit
-// LDS (the caller then uses the streaming kernel); *err holds launch errors.
-bool launch_resize2_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
-                         hipStream_t s, hipError_t *err);
-bool launch_resize2_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int wd,
-                        const float *lut, float *out, hipStream_t s, hipError_t *err);
-// One-wave-per-band resize (ldt_resize4.hip); false when unsupported (wide
-// taps or LDS), then the banded kernel above is used.
+// One-wave-per-band resize (ldt_resize4.hip); false when unsupported (taps
+// > 11, i.e. sources wider than 1120 px, or LDS), then the streaming
+// workgroup kernel (launch_resize_jpeg / launch_resize_raw) is used.
 bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
                          hipStream_t s, hipError_t *err);
 bool launch_resize4_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int wd,

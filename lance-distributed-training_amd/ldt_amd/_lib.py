@@ -44,7 +44,6 @@ OPT_PROFILE = 4
 OPT_RESIZE_IMPL = 5
 OPT_SUBSEQ_FIT = 6
 OPT_SYNC_WARM = 7
-OPT_DEBUG_SKIP = 8
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
 

@@ -12,10 +12,9 @@ call shapes as the reference's imports:
 * ``LanceDataset(path, batch_size, to_tensor_fn=..., sampler=...)`` — the
   iterable dataset of ``lance_iterable.py:53-59``.
 * ``SafeLanceDataset(uri)`` + ``get_safe_loader(...)`` — the map-style pair of
-  ``lance_map_style.py:54,60-69``. When the collate_fn is this build's GPU
-  collate, the DataLoader workers only fetch rows and the GPU decode runs in
-  the main process (``pin_memory`` is dropped: the outputs are device
-  tensors already).
+  ``lance_map_style.py:54,60-69``; ``get_safe_loader`` is a stock DataLoader.
+  With ``num_workers > 0`` the workers only fetch and pack rows; the GPU
+  decode runs in the main process (``ldt_amd.transforms.DeviceBatch``).
 
 It is I/O plumbing, not the accelerated path: the storage engine is out of
 scope.
@@ -183,13 +182,39 @@ class LanceDataset(IterableDataset):
         self.to_tensor_fn = to_tensor_fn
         self.batch_readahead = batch_readahead
 
-    def __iter__(self):
+    def _sampler(self):
         from .sampler import FullScanSampler
 
-        sampler = self.sampler or FullScanSampler()
-        batches = sampler(self.dataset, batch_size=self.batch_size, columns=self.columns,
-                          filter=self.filter, batch_readahead=self.batch_readahead)
+        return self.sampler or FullScanSampler()
+
+    def __getstate__(self):
+        # Pickled for DataLoader workers (spawn) in the main process: the
+        # sampler's batch plan is computed here, where the device kernels and
+        # the process group (pad=True's all_reduce) live, and the workers only
+        # read rows. Each worker w then yields plan batches w, w+nw, ... in
+        # order, which the DataLoader's round-robin turns back into the
+        # sampler's order.
+        state = dict(self.__dict__)
+        state["_worker_plan"] = self._sampler().read_plan(self.dataset, self.batch_size)
+        return state
+
+    def __iter__(self):
+        from torch.utils.data import get_worker_info
+
+        from .sampler import read_planned
+
+        info = get_worker_info()
         fn = self.to_tensor_fn
+        if info is not None:
+            plan = getattr(self, "_worker_plan", None)
+            if plan is None:  # not pickled (fork start method): plan in the worker
+                plan = self._sampler().read_plan(self.dataset, self.batch_size)
+            for desc in plan[info.id::info.num_workers]:
+                rb = read_planned(self.dataset, desc, self.columns)
+                yield fn(rb) if fn is not None else rb
+            return
+        batches = self._sampler()(self.dataset, batch_size=self.batch_size, columns=self.columns,
+                                  filter=self.filter, batch_readahead=self.batch_readahead)
         if fn is not None and getattr(fn, "prefetch", 0) > 0:
             # make_to_tensor_fn(prefetch=k): decode k batches ahead on side streams
             yield from fn.iterate(batches)
@@ -223,95 +248,15 @@ class SafeLanceDataset(Dataset):
         return self._d().take(list(indices), self.columns).to_pylist()
 
 
-def _pack_rows(rows):
-    """Worker side: the batch as torch tensors over the Arrow buffers (image
-    bytes, int32 offsets, labels), so DataLoader moves them through shared
-    memory instead of pickling megabytes through its result pipe."""
-    if not isinstance(rows, pa.RecordBatch):  # _ArrowRows fetched it packed already
-        from .transforms import pack_rows
-
-        rows = pack_rows(rows)
-    img = rows.column(rows.schema.get_field_index("image"))
-    if pa.types.is_large_binary(img.type):
-        img = img.cast(pa.binary())
-    off = np.frombuffer(img.buffers()[1], np.int32, len(img) + 1, img.offset * 4)
-    data = np.frombuffer(img.buffers()[2], np.uint8) if img.buffers()[2] is not None else np.zeros(0, np.uint8)
-    out = {"offsets": torch.from_numpy(off - off[0]),
-           "data": torch.from_numpy(data[off[0]:off[-1]].copy())}
-    if img.null_count:
-        out["valid"] = torch.from_numpy(np.asarray(img.is_valid()))
-    if "label" in rows.schema.names:
-        out["label"] = torch.from_numpy(rows.column(rows.schema.get_field_index("label")).to_numpy(zero_copy_only=False).astype(np.int64))
-    return out
-
-
-def _unpack_rows(packed) -> pa.RecordBatch:
-    """Main-process side of _pack_rows: an Arrow RecordBatch over the shared
-    tensors' memory (no copy)."""
-    n = packed["offsets"].numel() - 1
-    valid = None
-    if "valid" in packed:
-        valid = pa.array(packed["valid"].numpy()).buffers()[1]
-    img = pa.Array.from_buffers(pa.binary(), n, [valid, pa.py_buffer(packed["offsets"].numpy()),
-                                                  pa.py_buffer(packed["data"].numpy())])
-    cols, names = [img], ["image"]
-    if "label" in packed:
-        cols.append(pa.array(packed["label"].numpy()))
-        names.append("label")
-    return pa.RecordBatch.from_arrays(cols, names=names)
-
-
-class _ArrowRows(Dataset):
-    """SafeLanceDataset seen by get_safe_loader's workers when the collate runs
-    on the GPU: a batch of indices becomes one Arrow ``take`` (no per-row
-    Python dicts, which the GPU collate would only pack back into Arrow)."""
-
-    def __init__(self, ds: "SafeLanceDataset"):
-        self.ds = ds
-
-    def __len__(self) -> int:
-        return len(self.ds)
-
-    def __getitem__(self, i: int):
-        return self.ds[i]
-
-    def __getitems__(self, indices):
-        t = self.ds._d().take(list(indices), self.ds.columns).combine_chunks()
-        b = t.to_batches()
-        return b[0] if b else pa.RecordBatch.from_pylist([], schema=t.schema)
-
-
-class _DeviceCollateLoader:
-    """DataLoader whose workers fetch rows and pack them into one Arrow
-    RecordBatch per batch; the GPU collate runs in the main process (with
-    ``make_collate_fn(prefetch=k)``: k batches ahead on side streams)."""
-
-    def __init__(self, loader: DataLoader, collate_fn):
-        self.loader, self.collate_fn = loader, collate_fn
-
-    def __iter__(self):
-        pre = getattr(self.collate_fn, "_ldt_prefetch_iter", None)
-        batches = (_unpack_rows(p) for p in self.loader)
-        if pre is not None:
-            yield from pre(batches)
-            return
-        for rb in batches:
-            yield self.collate_fn(rb)
-
-    def __len__(self):
-        return len(self.loader)
-
-
 def get_safe_loader(dataset, batch_size: int, sampler=None, shuffle: bool = False, num_workers: int = 0,
                     collate_fn=None, pin_memory: bool = False, persistent_workers: bool = False, **kwargs):
-    """``lance.torch.data.get_safe_loader`` stand-in (lance_map_style.py:60-69)."""
-    device_collate = getattr(collate_fn, "_ldt_device_collate", False)
+    """``lance.torch.data.get_safe_loader`` stand-in (lance_map_style.py:60-69):
+    a stock ``torch.utils.data.DataLoader`` with spawn workers. The GPU
+    ``collate_fn`` needs no special casing: in the workers it packs the rows
+    into shared memory and the decode runs in the main process (see
+    ``ldt_amd.transforms.DeviceBatch``)."""
     mp_ctx = kwargs.pop("multiprocessing_context", "spawn" if num_workers > 0 else None)
-    if device_collate and isinstance(dataset, SafeLanceDataset):
-        dataset = _ArrowRows(dataset)
-    dl = DataLoader(dataset, batch_size=batch_size, sampler=sampler, shuffle=shuffle if sampler is None else False,
-                    num_workers=num_workers, collate_fn=_pack_rows if device_collate else collate_fn,
-                    pin_memory=False if device_collate else pin_memory,
-                    persistent_workers=persistent_workers if num_workers > 0 else False,
-                    multiprocessing_context=mp_ctx, **kwargs)
-    return _DeviceCollateLoader(dl, collate_fn) if device_collate else dl
+    return DataLoader(dataset, batch_size=batch_size, sampler=sampler, shuffle=shuffle if sampler is None else False,
+                      num_workers=num_workers, collate_fn=collate_fn, pin_memory=pin_memory,
+                      persistent_workers=persistent_workers if num_workers > 0 else False,
+                      multiprocessing_context=mp_ctx, **kwargs)

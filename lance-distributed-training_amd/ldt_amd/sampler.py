@@ -120,8 +120,14 @@ def _fragments(dataset):
     return dataset.get_fragments()
 
 
-def _read_range(dataset, start: int, end: int, columns) -> pa.RecordBatch:
-    return dataset.read_range(start, end, columns=columns)
+# A read plan is a list of picklable batch descriptors: ("range", start, end)
+# rows of the dataset, or ("frag", fragment, start, end) rows of one fragment.
+# Samplers compute the plan (device kernels, pad consensus) and read it with
+# read_planned; LanceDataset ships the plan to DataLoader workers.
+def read_planned(dataset, desc, columns=None) -> pa.RecordBatch:
+    if desc[0] == "range":
+        return dataset.read_range(desc[1], desc[2], columns=columns)
+    return _fragments(dataset)[desc[1]].read_slice(desc[2], desc[3], columns=columns)
 
 
 class _SamplerBase:
@@ -131,6 +137,18 @@ class _SamplerBase:
 
     def __repr__(self):
         return type(self).__name__
+
+    def read_plan(self, dataset, batch_size: int) -> list:
+        raise NotImplementedError
+
+    def __call__(self, dataset, *args, batch_size: int = 128, columns=None, filter=None,
+                 batch_readahead: int = 16, with_row_id=None, **kwargs) -> Iterator[pa.RecordBatch]:
+        """pylance sampler protocol: called by LanceDataset with the dataset and
+        batch size, yields the rank's RecordBatches."""
+        if filter is not None:
+            raise NotImplementedError("filter is not supported by the dataset shim")
+        for desc in self.read_plan(dataset, batch_size):
+            yield read_planned(dataset, desc, columns)
 
 
 class ShardedBatchSampler(_SamplerBase):
@@ -152,12 +170,8 @@ class ShardedBatchSampler(_SamplerBase):
             random.Random(self._seed).shuffle(r)
         return r
 
-    def __call__(self, dataset, *args, batch_size: int = 128, columns=None, filter=None,
-                 batch_readahead: int = 16, with_row_id=None, **kwargs) -> Iterator[pa.RecordBatch]:
-        if filter is not None:
-            raise NotImplementedError("filter is not supported by the dataset shim")
-        for (s, e) in self.ranges(dataset.count_rows(), batch_size):
-            yield _read_range(dataset, s, e, columns)
+    def read_plan(self, dataset, batch_size: int) -> list:
+        return [("range", s, e) for (s, e) in self.ranges(dataset.count_rows(), batch_size)]
 
 
 class ShardedFragmentSampler(_SamplerBase):
@@ -183,28 +197,21 @@ class ShardedFragmentSampler(_SamplerBase):
         recs, _ = self.compute_fragments(fragment_rows, batch_size, self._rank, self._world_size, target)
         return recs
 
-    def __call__(self, dataset, *args, batch_size: int = 128, columns=None, filter=None,
-                 batch_readahead: int = 16, with_row_id=None, **kwargs) -> Iterator[pa.RecordBatch]:
-        if filter is not None:
-            raise NotImplementedError("filter is not supported by the dataset shim")
+    def read_plan(self, dataset, batch_size: int) -> list:
         frags = _fragments(dataset)
         order = list(range(len(frags)))
         if self._randomize:
             random.Random(self._seed).shuffle(order)
         rows = [frags[i].count_rows() for i in order]
-        for (f, s, e, g, is_pad) in self.plan(rows, batch_size):
-            yield frags[order[f]].read_slice(s, e, columns=columns)
+        return [("frag", order[f], s, e) for (f, s, e, g, is_pad) in self.plan(rows, batch_size)]
 
 
 class FullScanSampler(_SamplerBase):
     """Every fragment on every rank (README.md:130-138). Not DDP-aware."""
 
-    def __call__(self, dataset, *args, batch_size: int = 128, columns=None, filter=None,
-                 batch_readahead: int = 16, with_row_id=None, **kwargs) -> Iterator[pa.RecordBatch]:
-        for frag in _fragments(dataset):
-            n = frag.count_rows()
-            for s in range(0, n, batch_size):
-                yield frag.read_slice(s, min(s + batch_size, n), columns=columns)
+    def read_plan(self, dataset, batch_size: int) -> list:
+        return [("frag", i, s, min(s + batch_size, f.count_rows()))
+                for i, f in enumerate(_fragments(dataset)) for s in range(0, f.count_rows(), batch_size)]
 
 
 class DistributedSampler(torch.utils.data.Sampler):

@@ -13,12 +13,22 @@ ToTensor -> stack``), bit-exact, except that the tensors are already on the
 GPU (``cuda:{LOCAL_RANK}``), so the consumer's ``.to(device)``
 (``lance_iterable.py:108-109``) is a no-op. All arithmetic runs in libldt.so's
 gfx950 kernels; Python only hands over Arrow buffer addresses.
+
+Inside a torch DataLoader worker (``num_workers > 0``: lance_map_style.py:60-69
+with 8 spawn workers, lance_iterable.py:71-72 under ``--no_ddp``) the workers
+never touch the GPU. There the plug-ins return a ``DeviceBatch``: the batch's
+compressed cells packed into shared-memory tensors, which the DataLoader moves
+to the main process. The GPU decode then runs in the main process — in the
+DataLoader's pin-memory thread when ``pin_memory=True`` (so it overlaps the
+training step), otherwise when the batch is first indexed. Decoded tensors are
+``DeviceTensor``s, whose ``pin_memory()`` is the identity, so
+``pin_memory=True`` also works when the collate runs in the main process.
 """
 from __future__ import annotations
 
 import ctypes
 import os
-from typing import Iterable, Optional, Sequence
+from typing import Iterable, Optional, Sequence, Tuple
 
 import numpy as np
 import pyarrow as pa
@@ -162,6 +172,155 @@ def decode_arrow(images: pa.Array, labels=None, *, device=None, normalize=None,
     return out, out_lbl
 
 
+class DeviceTensor(torch.Tensor):
+    """A decoded batch tensor on the GPU. Behaves as a plain ``torch.Tensor``
+    (ops on it return plain tensors); its ``pin_memory()`` returns itself, so
+    a DataLoader with ``pin_memory=True`` (lance_map_style.py:67) passes the
+    device tensors through instead of failing to pin them (torch pins dense
+    CPU tensors only)."""
+
+    __torch_function__ = torch._C._disabled_torch_function_impl
+
+    def pin_memory(self, device=None):
+        return self
+
+
+def _as_device_batch(img: torch.Tensor, lbl: Optional[torch.Tensor]) -> dict:
+    out = {"image": img.as_subclass(DeviceTensor)}
+    if lbl is not None:
+        out["label"] = lbl.as_subclass(DeviceTensor)
+    return out
+
+
+def _in_worker() -> bool:
+    """True inside a torch DataLoader worker process."""
+    return torch.utils.data.get_worker_info() is not None
+
+
+def _shm_uint8(nbytes: int) -> torch.Tensor:
+    t = torch.empty((nbytes,), dtype=torch.uint8)
+    t.share_memory_()  # the DataLoader then sends a handle, not the bytes
+    return t
+
+
+def _pack_list(images: Sequence, labels) -> dict:
+    """Worker side: a list of JPEG ``bytes`` (None = null cell) packed into one
+    shared-memory byte tensor + int64 offsets (one copy per cell)."""
+    n = len(images)
+    lens = np.fromiter((0 if b is None else len(b) for b in images), dtype=np.int64, count=n)
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    data = _shm_uint8(int(offs[-1]))
+    buf = data.numpy()
+    for i, b in enumerate(images):
+        if b:
+            buf[offs[i]:offs[i + 1]] = np.frombuffer(b, dtype=np.uint8)
+    packed = {"offsets": torch.from_numpy(offs), "data": data}
+    if any(b is None for b in images):
+        packed["valid"] = torch.from_numpy(np.fromiter((b is not None for b in images), dtype=np.bool_, count=n))
+    if labels is not None:
+        packed["label"] = torch.from_numpy(np.ascontiguousarray(np.asarray(labels, dtype=np.int64)))
+    return packed
+
+
+def _pack_arrow(images: pa.Array, labels) -> dict:
+    """Worker side: an Arrow ``binary``/``large_binary`` column (any offset)
+    packed like ``_pack_list`` with one memcpy of its data range."""
+    if isinstance(images, pa.ChunkedArray):
+        images = images.combine_chunks()
+    n = len(images)
+    bufs = images.buffers()
+    odt = np.int64 if pa.types.is_large_binary(images.type) or pa.types.is_large_string(images.type) else np.int32
+    offs = np.frombuffer(bufs[1], dtype=odt, count=n + 1, offset=images.offset * np.dtype(odt).itemsize)
+    offs = offs.astype(np.int64)
+    lo, hi = int(offs[0]), int(offs[-1])
+    data = _shm_uint8(hi - lo)
+    if hi > lo:
+        data.numpy()[:] = np.frombuffer(bufs[2], dtype=np.uint8, count=hi - lo, offset=lo)
+    packed = {"offsets": torch.from_numpy(offs - lo), "data": data}
+    if images.null_count:
+        packed["valid"] = torch.from_numpy(np.asarray(images.is_valid().to_numpy(zero_copy_only=False), np.bool_))
+    if labels is not None:
+        packed["label"] = torch.from_numpy(np.ascontiguousarray(labels, dtype=np.int64))
+    return packed
+
+
+def _unpack(packed: dict) -> Tuple[pa.Array, Optional[np.ndarray]]:
+    """Main-process side: a ``large_binary`` Arrow array over the shared
+    tensors (no copy) and the labels."""
+    offs = packed["offsets"].numpy()
+    n = len(offs) - 1
+    valid = None
+    if "valid" in packed:
+        valid = pa.array(packed["valid"].numpy()).buffers()[1]
+    data = packed["data"].numpy()
+    arr = pa.Array.from_buffers(pa.large_binary(), n, [valid, pa.py_buffer(offs), pa.py_buffer(data)])
+    lab = packed["label"].numpy() if "label" in packed else None
+    return arr, lab
+
+
+class DeviceBatch:
+    """What ``collate_fn`` / ``decode_tensor_image`` return inside a DataLoader
+    worker: the batch's compressed cells in shared memory, decoded on the GPU
+    in the main process on first use.
+
+    Indexing (``batch["image"]``, ``batch["label"]``), ``keys()``/``items()``
+    and ``pin_memory()`` trigger the decode; ``pin_memory()`` — called by the
+    DataLoader's pin-memory thread when ``pin_memory=True`` — returns the plain
+    ``{"image", "label"}`` dict. Deliberately not a ``Mapping``: torch's
+    ``pin_memory`` would otherwise pin the values one by one instead of calling
+    ``pin_memory()`` on the batch. Decode errors raise ``ImageDecodeError``
+    where the decode runs (re-raised in the main thread by the DataLoader when
+    it runs in the pin-memory thread)."""
+
+    __slots__ = ("_packed", "_device", "_normalize", "_out")
+
+    def __init__(self, packed: dict, device=None, normalize=None):
+        self._packed = packed
+        self._device = None if device is None else str(device)
+        self._normalize = normalize
+        self._out = None
+
+    def decode(self) -> dict:
+        if self._out is None:
+            arr, lab = _unpack(self._packed)
+            img, lbl = decode_arrow(arr, lab, device=self._device, normalize=self._normalize)
+            self._out = _as_device_batch(img, lbl)
+            self._packed = None
+        return self._out
+
+    def pin_memory(self, device=None) -> dict:
+        return self.decode()
+
+    def __getitem__(self, key):
+        return self.decode()[key]
+
+    def __contains__(self, key) -> bool:
+        return key in self.decode()
+
+    def __iter__(self):
+        return iter(self.decode())
+
+    def __len__(self) -> int:
+        return len(self.decode())
+
+    def keys(self):
+        return self.decode().keys()
+
+    def values(self):
+        return self.decode().values()
+
+    def items(self):
+        return self.decode().items()
+
+    def get(self, key, default=None):
+        return self.decode().get(key, default)
+
+    def __repr__(self) -> str:
+        state = "decoded" if self._out is not None else f"{len(self._packed['offsets']) - 1} cells pending"
+        return f"DeviceBatch({state})"
+
+
 def decode_tensor_image(batch, **kwargs):
     """to_tensor_fn: ``pa.RecordBatch`` -> ``{"image", "label"}`` (lance_iterable.py:38-50).
 
@@ -169,69 +328,58 @@ def decode_tensor_image(batch, **kwargs):
     the reference's ``**kwargs`` does. Optional keywords of this build:
     ``image_column`` ("image"), ``label_column`` ("label"), ``device``,
     ``normalize`` (False; True = ImageNet mean/std, lance_iterable.py:31).
+    In a DataLoader worker it returns a ``DeviceBatch`` (decoded in the main
+    process).
     """
     image_column = kwargs.get("image_column", "image")
     label_column = kwargs.get("label_column", "label")
     images = _column(batch, image_column)
+    if _in_worker():
+        labels = None
+        if label_column is not None and label_column in batch.schema.names:
+            lab = _column(batch, label_column)
+            if lab.null_count:
+                raise ValueError(f"null values in label column {label_column!r}")
+            labels = lab.to_numpy(zero_copy_only=False)
+        return DeviceBatch(_pack_arrow(images, labels), kwargs.get("device"), kwargs.get("normalize"))
     lab = _labels_buffer(batch, label_column)
     img, lbl = decode_arrow(images, lab, device=kwargs.get("device"),
                             normalize=kwargs.get("normalize"), stream=kwargs.get("stream"))
-    out = {"image": img}
-    if lbl is not None:
-        out["label"] = lbl
-    return out
+    return _as_device_batch(img, lbl)
 
 
 def collate_fn(batch_of_dicts, *, device=None, normalize=None):
     """collate_fn: list of ``{"image": bytes, "label": int}`` -> stacked tensors
-    (lance_map_style.py:21-44). The bytes are packed into one Arrow buffer
-    (zero-copy of the Python ``bytes`` objects is impossible; this is the one
-    host copy) and decoded on the GPU. get_safe_loader's workers may hand over
-    the rows already packed as a ``pa.RecordBatch`` (``pack_rows``)."""
+    (lance_map_style.py:21-44). The bytes are packed into one buffer (zero-copy
+    of the Python ``bytes`` objects is impossible; this is the one host copy)
+    and decoded on the GPU — in a DataLoader worker, packed into shared memory
+    and returned as a ``DeviceBatch`` for the main process to decode. A
+    ``pa.RecordBatch`` is accepted too."""
     if isinstance(batch_of_dicts, pa.RecordBatch):
         return decode_tensor_image(batch_of_dicts, device=device, normalize=normalize)
     images = [item["image"] for item in batch_of_dicts]
-    labels = [item["label"] for item in batch_of_dicts]
+    labels = [item["label"] for item in batch_of_dicts] if batch_of_dicts and "label" in batch_of_dicts[0] \
+        else None
+    if _in_worker():
+        return DeviceBatch(_pack_list(images, labels), device, normalize)
     arr = pa.array(images, type=pa.binary())
     img, lbl = decode_arrow(arr, labels, device=device, normalize=normalize)
-    return {"image": img, "label": lbl}
+    return _as_device_batch(img, lbl)
 
 
-def pack_rows(batch_of_dicts) -> pa.RecordBatch:
-    """DataLoader-worker side of the GPU collate: the rows' bytes and labels
-    as one Arrow RecordBatch (pickled as a few buffers instead of one Python
-    object per row)."""
-    cols = [pa.array([item["image"] for item in batch_of_dicts], type=pa.binary())]
-    names = ["image"]
-    if batch_of_dicts and "label" in batch_of_dicts[0]:
-        cols.append(pa.array([item["label"] for item in batch_of_dicts], type=pa.int64()))
-        names.append("label")
-    return pa.RecordBatch.from_arrays(cols, names=names)
+def make_collate_fn(device=None, normalize=None):
+    """A picklable collate_fn bound to a device / Normalize setting (for
+    ``DataLoader(collate_fn=...)`` with spawn workers)."""
+    return _BoundCollate(device, normalize)
 
 
-collate_fn._ldt_device_collate = True  # get_safe_loader: decode in the main process
+class _BoundCollate:
+    def __init__(self, device, normalize):
+        self.device = None if device is None else str(device)
+        self.normalize = normalize
 
-
-def make_collate_fn(device=None, normalize=None, prefetch: int = 0, depth: int = 3):
-    """A collate_fn bound to a device / Normalize setting.
-
-    ``prefetch=k`` (k < depth): ``get_safe_loader`` then decodes k batches ahead
-    on a ``DecodePipeline`` (the workers' next batches decode while the consumer
-    uses the current one); per-image errors surface asynchronously, as with
-    ``make_to_tensor_fn(prefetch=k)``."""
-    def _fn(batch_of_dicts):
-        return collate_fn(batch_of_dicts, device=device, normalize=normalize)
-    _fn._ldt_device_collate = True
-    if prefetch > 0:
-        state = {}
-
-        def _iterate(record_batches):
-            if "pipe" not in state:
-                state["pipe"] = DecodePipeline(depth=depth, device=device)
-            return state["pipe"].prefetch(record_batches, ahead=min(prefetch, depth - 1), normalize=normalize)
-
-        _fn._ldt_prefetch_iter = _iterate
-    return _fn
+    def __call__(self, batch_of_dicts):
+        return collate_fn(batch_of_dicts, device=self.device, normalize=self.normalize)
 
 
 def resize_raw(hwc, height: int, width: int, *, device=None, normalize=True):
@@ -401,26 +549,29 @@ class DecodePipeline:
         batches enqueued before each yield: while the consumer's step k runs on
         torch's stream, batches k+1..k+ahead decode on the slots' streams
         (decode overlapped with the training step, so
-        ``.to(device)`` at lance_iterable.py:108-109 is a no-op). Per-image
-        errors surface when a slot is reused or at the end."""
+        ``.to(device)`` at lance_iterable.py:108-109 is a no-op). A batch's
+        per-image status is checked before it is yielded: ImageDecodeError is
+        raised instead of yielding a batch with a failed row."""
         from collections import deque
 
         ahead = max(0, min(int(ahead), self.depth - 1))
         q = deque()
 
         def emit():
-            img, lbl, ready = q.popleft()
+            img, lbl, ready, slot = q.popleft()
+            # the batch's own slot is checked before it is yielded, so a bad
+            # row raises here (as PIL would) instead of reaching the consumer;
+            # it waits only for this batch, enqueued `ahead` batches ago
+            self.check_slot(slot)
             ready()
-            out = {"image": img}
-            if lbl is not None:
-                out["label"] = lbl
-            return out
+            return _as_device_batch(img, lbl)
 
         for b in batches:
             if self.k >= self.depth:
                 self.check_slot(self.k % self.depth)
+            slot = self.k % self.depth
             q.append(self.decode(b, normalize=normalize, image_column=image_column,
-                                 label_column=label_column, wait=False))
+                                 label_column=label_column, wait=False) + (slot,))
             if len(q) > ahead:
                 yield emit()
         while q:
@@ -480,10 +631,7 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
         img, lbl = pipe.decode(batch, normalize=kwargs.get("normalize", normalize),
                                image_column=kwargs.get("image_column", fixed.get("image_column", "image")),
                                label_column=kwargs.get("label_column", fixed.get("label_column", "label")))
-        out = {"image": img}
-        if lbl is not None:
-            out["label"] = lbl
-        return out
+        return _as_device_batch(img, lbl)
 
     to_tensor_fn.check = pipe.check
     to_tensor_fn.pipeline = pipe

@@ -30,7 +30,7 @@
  * The third-party sources are not in the container; this is a
  * restatement of their published algorithms, pinned bit-exact against the
  * Pillow/libjpeg-turbo binaries present here by tests/golden (see
- * tests/golden/make_golden.py and tests/test_oracle_golden.py).
+ * tests/golden/make_golden.py and tests/test_oracle.py).
  *
  * Plain C99, scalar, single-threaded.
  */

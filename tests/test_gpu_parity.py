@@ -518,40 +518,6 @@ def test_prefetching_to_tensor_fn_overlaps_and_matches(tmp_path):
         assert torch.equal(a["image"], b["image"])
 
 
-def test_map_style_loader_prefetch_matches_sync(tmp_path):
-    """get_safe_loader + DistributedSampler (lance_map_style.py:54-69) with the
-    GPU collate: workers pack rows into RecordBatches; make_collate_fn(prefetch=2)
-    yields the same tensors as the synchronous collate_fn, in sampler order."""
-    import torch
-
-    import ldt_amd
-    from ldt_amd import synth
-
-    cells, labels = synth.food101_like(200, seed=9)
-    path = str(tmp_path / "ds")
-    ldt_amd.write_dataset(pa.table({"image": pa.array(cells, pa.binary()), "label": pa.array(labels, pa.int64())}),
-                          path, max_rows_per_file=64)
-    ds = ldt_amd.SafeLanceDataset(path)
-    outs = []
-    for collate in (ldt_amd.collate_fn, ldt_amd.make_collate_fn(prefetch=2)):
-        smp = ldt_amd.DistributedSampler(ds, num_replicas=1, rank=0, seed=1)
-        smp.set_epoch(4)
-        loader = ldt_amd.get_safe_loader(ds, batch_size=48, sampler=smp, num_workers=2, collate_fn=collate)
-        outs.append([{k: v.clone() for k, v in b.items()} for b in loader])
-    assert len(outs[0]) == len(outs[1]) == 5
-    order = list(torch.utils.data.DistributedSampler(range(200), num_replicas=1, rank=0, seed=1).__iter__())
-    for a, b in zip(*outs):
-        assert torch.equal(a["image"], b["image"]) and torch.equal(a["label"], b["label"])
-    # spot-check one row against the oracle, in the sampler's order
-    from oracle import oracle
-    t = torch.utils.data.DistributedSampler(range(200), num_replicas=1, rank=0, seed=1)
-    t.set_epoch(4)
-    first = list(t)[0]
-    assert np.array_equal(outs[1][0]["image"][0].cpu().numpy(), oracle.jpeg_to_tensor(cells[first]))
-    assert int(outs[1][0]["label"][0]) == int(labels[first])
-    del order
-
-
 def _sos_end(b: bytes) -> int:
     """Offset of the first entropy-coded byte (after the first SOS header)."""
     i = 2
