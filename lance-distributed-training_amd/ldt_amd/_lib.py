@@ -66,9 +66,15 @@ class ImageDecodeError(ValueError, OSError):
     Subclasses OSError so code written against the reference (PIL raises
     UnidentifiedImageError / OSError from Image.open at lance_iterable.py:42)
     keeps working, and ValueError per SURVEY.md §8b. ``rows`` maps row index ->
-    LDT_IMG_* status."""
+    LDT_IMG_* status. Also constructible from a message string alone, which is
+    how torch's DataLoader re-raises an exception caught in a worker or in the
+    pin-memory thread (``ExceptionWrapper.reraise``)."""
 
-    def __init__(self, rows: dict):
+    def __init__(self, rows):
+        if isinstance(rows, str):
+            self.rows = {}
+            super().__init__(rows)
+            return
         self.rows = dict(rows)
         first = sorted(self.rows)[:8]
         desc = "; ".join(f"row {i}: {IMG_STATUS_TEXT.get(self.rows[i], self.rows[i])}" for i in first)

@@ -127,3 +127,17 @@ def test_distributed_sampler_rank_errors():
         DistributedSampler(range(5), num_replicas=2, rank=2)
     with pytest.raises(ValueError):
         DistributedSampler(range(5), num_replicas=2, rank=-1)
+
+
+def test_image_decode_error_survives_dataloader_reraise():
+    """torch re-raises worker / pin-thread exceptions as exc_type(message)."""
+    from torch._utils import ExceptionWrapper
+
+    from ldt_amd import ImageDecodeError
+
+    try:
+        raise ImageDecodeError({1: 3})
+    except ImageDecodeError:
+        w = ExceptionWrapper(where="in pin memory thread for device 0")
+    with pytest.raises(ImageDecodeError, match="row 1"):
+        w.reraise()
