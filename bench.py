@@ -172,13 +172,11 @@ def main():
         comp_bytes = float(np.mean([len(c) for c in cells_all]))
         it = [0]
         pipe = ldt_amd.DecodePipeline(depth=args.depth, device=dev, profile=not args.no_stage_events)
-        for c in pipe.ctxs:  # tuning knobs (defaults: S = 1024 bits, fitted per image)
+        for c in pipe.ctxs:  # tuning knobs (default minimum S = 256 bits, fitted per image)
             if os.environ.get("LDT_SUBSEQ_BITS"):
                 c.set_option(_lib.OPT_SUBSEQ_BITS, int(os.environ["LDT_SUBSEQ_BITS"]))
             if os.environ.get("LDT_SYNC_WARM"):
                 c.set_option(_lib.OPT_SYNC_WARM, int(os.environ["LDT_SYNC_WARM"]))
-            if os.environ.get("LDT_SUBSEQ_FIT"):
-                c.set_option(_lib.OPT_SUBSEQ_FIT, int(os.environ["LDT_SUBSEQ_FIT"]))
 
         def step():
             b = batches[it[0] % nb]

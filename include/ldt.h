@@ -56,18 +56,19 @@ extern "C" {
                                  report device-side per-image errors before
                                  returning; 0: asynchronous, errors are read
                                  later with ldt_fetch_status()                  */
-#define LDT_OPT_HUFF_MODE 2   /* 0 auto (default), 1 serial per segment,
-                                 2 parallel self-synchronising subsequences     */
-#define LDT_OPT_SUBSEQ_BITS 3 /* subsequence length for mode 2: 64..2048 bits,
-                                 multiple of 32 (default 1024)                  */
+#define LDT_OPT_HUFF_MODE 2   /* 0 auto (default) and 2: the parallel
+                                 self-synchronising decoder, one workgroup per
+                                 image (the serial one for images with > 512
+                                 restart segments); 1: serial per segment      */
+#define LDT_OPT_SUBSEQ_BITS 3 /* minimum subsequence length of the parallel
+                                 decoder: 64..8192 bits, multiple of 32
+                                 (default 256); each image uses the smallest
+                                 S >= this that fits its slots in 1024 lanes   */
 #define LDT_OPT_PROFILE 4     /* 1: record HIP events around every stage on the
                                  caller's stream (read with ldt_stage_times)    */
 #define LDT_OPT_RESIZE_IMPL 5 /* 0 auto (default): one wave per band; 2: the
                                  streaming workgroup kernel that serves sources
                                  wider than 1120 px (cross-check)               */
-#define LDT_OPT_SUBSEQ_FIT 6  /* 1 (default): per image, shrink the subsequence
-                                 length so its slots fill whole workgroups;
-                                 0: every image uses LDT_OPT_SUBSEQ_BITS        */
 #define LDT_OPT_SYNC_WARM 7   /* parallel decoder phase 1 starts this % of S
                                  before each range (0..200, default 0)         */
 

@@ -128,10 +128,9 @@ struct ldt_ctx {
   bool sync_status = true;
   int huff_mode = 0;
   int resize_impl = 0;
-  bool subseq_fit = true;
   int warm_pct = 0;
-  int subseq_bits = 1024;
-  DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_sub, d_pre, d_dscnt;
+  int subseq_bits = 256; // minimum S of the parallel decoder
+  DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_dscnt;
   DevBuf d_perm; // DistributedSampler scratch: 3 int32 arrays of dataset_len
   std::unique_ptr<CopyPool> copier; // host -> pinned copies (created on first use)
   static constexpr int kSlots = 2;
@@ -334,12 +333,12 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   int64_t dst_total = 0, coef_blocks = 0, plane_total = 0, max_blocks = 0;
   const bool parallel = c->huff_mode != 1;
   const int SB = c->subseq_bits;
-  int32_t n_wg = 0;
-  std::vector<int32_t> wg_img;
+  std::vector<int32_t> par_img; // images on the parallel decoder (one workgroup each)
+  int n_serial = 0;
+  int64_t max_window = 0;       // largest LDS window a parallel image needs
   int32_t n_chunks = 0;          // destuff chunks (kDsChunk bytes of scan data each)
   std::vector<int32_t> chunk_img;
   int max_w = 1, max_h = 1, max_ks_h = 3, max_ks_v = 3, max_tabs = 1, n_fast420 = 0;
-  int max_sub_bits = 64; // largest per-image S: sizes the decoders' LDS window
   std::vector<ProgScan> pscans;  // progressive images' scans (k_prog)
   std::vector<ProgTab> ptabs;
   std::unordered_map<std::string, int> ptab_map;
@@ -505,7 +504,6 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       plane_total = pl;
       d.restart = 0;
       d.nseg = 0;
-      d.wg_first = n_wg;
       d.ds_first = n_chunks;
       d.dst_off = dst_total;
       d.prog_first = (int32_t)pscans.size();
@@ -569,30 +567,23 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     }
     d.src_off = ip.cell_off + H.scan_pos;
     d.src_len = ip.cell_len - H.scan_pos;
-    if (parallel) {
-      // subsequence length of this image: without restart markers, the largest
-      // S <= the context's S that still fills its last workgroup (fewer,
-      // fuller workgroups; S stays within the LDS window sized for SB)
-      int64_t sbits = SB;
-      if (c->subseq_fit && d.nseg == 1 && SB >= 256) {
-        const int64_t bits = d.src_len * 8;
-        const int64_t k = std::max<int64_t>(1, (bits + (int64_t)SB * (kSlotsPerWg - 1) - 1) /
-                                                   ((int64_t)SB * (kSlotsPerWg - 1)));
-        sbits = (bits + k * (kSlotsPerWg - 1) - 1) / (k * (kSlotsPerWg - 1));
-        sbits = std::min<int64_t>(SB, std::max<int64_t>(256, (sbits + 31) & ~(int64_t)31));
-      }
+    if (parallel && d.nseg <= kMaxParSegs) {
+      // k_huff_image: all of the image's slots in one workgroup. Slots are
+      // sum over segments of ceil(bits_s / S) <= bits / S + nseg, so
+      // S >= bits / (kHuffThreads - nseg) fits; the option is a lower bound.
+      const int64_t bits = d.src_len * 8;
+      const int64_t room = kHuffThreads - d.nseg;
+      int64_t sbits = std::max<int64_t>((bits + room - 1) / room, std::max(SB, 64));
+      sbits = (sbits + 31) & ~(int64_t)31;
       // an odd number of 32-bit words per range: lanes' LDS window reads start
-      // in distinct banks (the window is not skewed)
-      if (((sbits >> 5) & 1) == 0 && sbits >= 256) sbits = sbits + 32 <= SB ? sbits + 32 : sbits - 32;
+      // in distinct banks
+      if (((sbits >> 5) & 1) == 0) sbits += 32;
       d.sub_bits = (int32_t)sbits;
-      if (sbits > max_sub_bits) max_sub_bits = (int)sbits;
-      // subsequence slots: sum over segments of ceil(bits_s / S) <= bits / S + nseg
-      const int64_t slots = (d.src_len * 8 + sbits - 1) / sbits + d.nseg;
-      d.wg_count = (int32_t)((slots + kSlotsPerWg - 1) / kSlotsPerWg);
-      d.wg_first = n_wg;
-      d.sub_cap = d.wg_count * kSlotsPerWg;
-      for (int q = 0; q < d.wg_count; ++q) wg_img.push_back((int32_t)i);
-      n_wg += d.wg_count;
+      par_img.push_back((int32_t)i);
+      max_window = std::max<int64_t>(max_window, destuff_region_bytes(d.src_len, d.nseg) + 16);
+    } else {
+      d.sub_bits = 0;
+      ++n_serial;
     }
     // destuff chunks over the scan bytes from the 4-aligned word before them
     d.ds_first = n_chunks;
@@ -600,7 +591,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     for (int q = 0; q < d.ds_count; ++q) chunk_img.push_back((int32_t)i);
     n_chunks += d.ds_count;
     d.dst_off = dst_total;
-    dst_total += align_up(d.src_len + 16 + (int64_t)kSegPad * d.nseg, 16);
+    dst_total += destuff_region_bytes(d.src_len, d.nseg);
     } // !progressive
     d.coef_off = coef_blocks;
     const int64_t nblk = nmcu * d.bpm;
@@ -637,7 +628,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   const int64_t off_status = off;
   off = align_up(off + 4 * n, 64);
   const int64_t off_wg = off;
-  off = align_up(off + 4 * (int64_t)n_wg, 64);
+  off = align_up(off + 4 * (int64_t)par_img.size(), 64);
   const int64_t off_chunk = off;
   off = align_up(off + 4 * (int64_t)n_chunks, 64);
   const int64_t off_redo = off;
@@ -669,7 +660,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   build_lut(norm, reinterpret_cast<float *>(hp + ph.off_lut));
   if (labels) memcpy(hp + ph.off_labels, labels + label_offset, 8 * (size_t)n);
   memcpy(hp + off_status, st.data(), 4 * (size_t)n);
-  if (n_wg) memcpy(hp + off_wg, wg_img.data(), 4 * (size_t)n_wg);
+  if (!par_img.empty()) memcpy(hp + off_wg, par_img.data(), 4 * par_img.size());
   if (n_chunks) memcpy(hp + off_chunk, chunk_img.data(), 4 * (size_t)n_chunks);
   memset(hp + off_redo, 0, 64);
   if (!pscans.empty()) memcpy(hp + off_pscan, pscans.data(), sizeof(ProgScan) * pscans.size());
@@ -685,11 +676,6 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if ((rc = ensure_dev(c, c->d_dcv, (size_t)coef_blocks * 2 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dscnt, 16 * (size_t)(n_chunks + 1), s))) return rc;
-  if (parallel && n_wg) {
-    const size_t slots = (size_t)n_wg * kSyncThreads;
-    if ((rc = ensure_dev(c, c->d_sub, slots * sizeof(SubState), s))) return rc;
-    if ((rc = ensure_dev(c, c->d_pre, slots * 4, s))) return rc;
-  }
   prof_begin(c, LDT_STAGE_H2D, s);
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
@@ -720,10 +706,17 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.max_w = max_w;
   p.max_h = max_h;
   p.max_blocks = max_blocks;
-  p.subseq_bits = parallel ? max_sub_bits : 0;
+  p.n_par = (int)par_img.size();
+  p.par_img = reinterpret_cast<const int32_t *>(dp + off_wg);
+  p.n_serial = n_serial;
+  {
+    // LDS window of k_huff_image: the largest image's stream, capped by what
+    // is left of the CU's LDS after the tables (bigger streams read global)
+    const int64_t cap =
+        kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs) - huff_cnt_lds(max_tabs);
+    p.win_bytes = (int)(std::min<int64_t>(max_window, cap) & ~(int64_t)15);
+  }
   p.warm_pct = c->warm_pct;
-  p.n_wg = parallel ? n_wg : 0;
-  p.wg_img = reinterpret_cast<const int32_t *>(dp + off_wg);
   p.n_chunks = n_chunks;
   p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
   p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
@@ -741,14 +734,12 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.dcv = static_cast<int16_t *>(c->d_dcv.p);
   w.planes = static_cast<uint8_t *>(c->d_planes.p);
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
-  w.sub = static_cast<SubState *>(c->d_sub.p);
   w.ds_cnt = static_cast<int4 *>(c->d_dscnt.p);
-  w.sub_pre = static_cast<int32_t *>(c->d_pre.p);
 
   HIPCHK(c, launch_destuff(p, w, s));
   prof_mark(c, LDT_STAGE_DESTUFF, s);
-  if (parallel) HIPCHK(c, launch_huff_parallel(p, w, s));
-  else HIPCHK(c, launch_huff_serial(p, w, s));
+  HIPCHK(c, launch_huff_parallel(p, w, s));
+  HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_prog(p, w, s));
   HIPCHK(c, launch_dc_scan(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
@@ -829,7 +820,7 @@ void ldt_destroy(ldt_ctx *c) {
   DeviceGuard g(c->device);
   (void)hipDeviceSynchronize();
   DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_dcv,
-                    &c->d_planes, &c->d_raw, &c->d_sub, &c->d_pre, &c->d_dscnt};
+                    &c->d_planes, &c->d_raw, &c->d_dscnt};
   for (DevBuf *b : dbs)
     if (b->p) (void)hipFree(b->p);
   for (int k = 0; k < ldt_ctx::kSlots; ++k) {
@@ -861,15 +852,12 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     if (value < 0 || value > 200) return set_err(c, LDT_ERR_ARG, "sync warm-up %lld", (long long)value);
     c->warm_pct = (int)value;
     return LDT_OK;
-  case LDT_OPT_SUBSEQ_FIT:
-    c->subseq_fit = value != 0;
-    return LDT_OK;
   case LDT_OPT_RESIZE_IMPL:
     if (value != 0 && value != 2) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
     c->resize_impl = (int)value;
     return LDT_OK;
   case LDT_OPT_SUBSEQ_BITS:
-    if (value < 64 || value > 2048 || (value & 31))
+    if (value < 64 || value > 8192 || (value & 31))
       return set_err(c, LDT_ERR_ARG, "subsequence bits %lld", (long long)value);
     c->subseq_bits = (int)value;
     return LDT_OK;

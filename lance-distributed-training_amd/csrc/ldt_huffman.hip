@@ -16,11 +16,14 @@
 // bit-field extract and one add move the state (see ldt_types.hpp).
 //
 // Two decoders share it:
-//   k_huff_serial    one workgroup per image, one lane per segment;
-//   k_huff_sync/fix/scan/write   the self-synchronising parallel decoder
-//                    (Weissenberger & Schmidt, ICPP 2018), see below.
+//   k_huff_serial    one workgroup per image, one lane per segment (images
+//                    with many restart segments, or LDT_OPT_HUFF_MODE 1);
+//   k_huff_image     the self-synchronising parallel decoder (Weissenberger &
+//                    Schmidt, ICPP 2018), one 1024-lane workgroup per image.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "ldt_device.hpp"
 #include "ldt_kernels.hpp"
@@ -110,9 +113,12 @@ struct Rd {
 // ---------------------------------------------------------------------------
 struct Dec {
   lds_cu16 tabs;     // the image's distinct tables, kTabU16 entries per slot
+  const LDS_AS uint32_t *cnt; // count-mode tables, 2^kLookBits entries per slot (k_huff_image)
   uint32_t dcseq;    // LDS table slot of MCU block b's DC table at bits 3b
   uint32_t acseq;    // ... AC table
   int b3end;         // 3 * blocks per MCU
+  int ns;            // distinct tables (slots)
+  uint32_t acmask;   // slots holding AC tables
   const HuffTab *g;  // plan tables (canonical fallback)
   const ImgDesc *d;
 };
@@ -167,12 +173,16 @@ __device__ __forceinline__ Dec load_dec(const ImgDesc &d, const HuffTab *__restr
   }
   Dec dec;
   dec.tabs = tabs;
+  dec.cnt = nullptr;
   dec.dcseq = dec.acseq = 0;
   for (int b = 0; b < d.bpm; ++b) {
     const int c = d.bcomp[b] & 3;
     dec.dcseq |= ((slotmap >> (6 * c)) & 7) << (3 * b);
     dec.acseq |= ((slotmap >> (6 * c + 3)) & 7) << (3 * b);
   }
+  dec.ns = ns;
+  dec.acmask = 0;
+  for (int x = 1; x < 6; x += 2) dec.acmask |= 1u << ((slotmap >> (3 * x)) & 7);
   dec.b3end = 3 * d.bpm;
   dec.g = htabs;
   dec.d = &d;
@@ -227,14 +237,73 @@ __device__ __forceinline__ void advance(St &st, const Dec &dec, int adv) {
   st.k = end ? 0 : k2;
 }
 
-// Count-only symbol: blocks started.
+// Count-mode tables (k_huff_image's sync passes only count blocks, so one
+// lookup may consume several symbols). Entry for each kLookBits-bit peek:
+//   T (bits 0-4)     bits of the longest run of AC symbols of one block whose
+//                    codes all lie in the peeked bits (the last symbol's
+//                    magnitude may extend past them)
+//   ADV (5-11)       coefficient advance of the whole run (EOB 64 ends it)
+//   PRE (12-18)      advance before the run's last symbol: the run is valid
+//                    only if k + PRE < 64 (no block ends inside it)
+//   t1, adv1 (19-23, 24-30)  the first symbol alone
+// DC tables hold single symbols. T == 0: a long code, the entry is the kTabU16
+// table's indirect entry (second level / canonical search).
+__device__ __forceinline__ void build_count_tables(const Dec &dec, LDS_AS uint32_t *cnt, int tid,
+                                                   int nthreads) {
+  constexpr uint32_t kMask = (1u << kLookBits) - 1;
+  for (int i = tid; i < (dec.ns << kLookBits); i += nthreads) {
+    const int q = i >> kLookBits;
+    const uint32_t x = (uint32_t)i & kMask;
+    const lds_cu16 tb = dec.tabs + q * kTabU16;
+    const uint32_t e = tb[x];
+    const uint32_t t1 = e & 31;
+    uint32_t c = e; // indirect: as the kTabU16 entry
+    if (t1 != 0) {
+      const uint32_t adv1 = e >> 9;
+      uint32_t T = t1, ADV = adv1, PRE = 0;
+      if ((dec.acmask >> q) & 1) {
+        while (ADV < 64 && T < (uint32_t)kLookBits) {
+          const uint32_t e2 = tb[(x << T) & kMask];
+          const uint32_t t2 = e2 & 31;
+          if (t2 == 0) break;
+          const uint32_t cl2 = t2 - ((e2 >> 5) & 15); // code length
+          if (T + cl2 > (uint32_t)kLookBits || ADV >= 63) break;
+          PRE = ADV;
+          ADV += e2 >> 9;
+          T += t2;
+        }
+      }
+      c = T | (ADV << 5) | (PRE << 12) | (t1 << 19) | (adv1 << 24);
+    }
+    cnt[i] = c;
+  }
+}
+
+// Count-only step (blocks started): one count-table lookup, one or more symbols.
 template <class W>
 __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int &nblk) {
   const uint32_t pk = R.peek();
-  const uint32_t e = lookup(dec, st, pk);
+  const bool ac = st.k != 0;
+  const uint32_t slot = __builtin_amdgcn_ubfe(ac ? dec.acseq : dec.dcseq, (uint32_t)st.b3, 3u);
+  const uint32_t c = dec.cnt[(slot << kLookBits) + (pk >> (32 - kLookBits))];
+  uint32_t t, adv;
+  if (__builtin_expect((c & 31) == 0, 0)) {
+    const lds_cu16 tb = dec.tabs + slot * kTabU16;
+    uint32_t e;
+    if (c != kHuffCanon)
+      e = tb[(1 << kLookBits) + ((c >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
+    else
+      e = lookup_canon(dec.g, dec.d, st.b3 / 3, ac, pk);
+    t = e & 31;
+    adv = e >> 9;
+  } else {
+    const bool ok = (uint32_t)st.k + ((c >> 12) & 127) < 64;
+    t = ok ? (c & 31) : ((c >> 19) & 31);
+    adv = ok ? ((c >> 5) & 127) : (c >> 24);
+  }
   nblk += st.k == 0 ? 1 : 0;
-  R.consume((int)(e & 31));
-  advance(st, dec, (int)(e >> 9));
+  R.consume((int)t);
+  advance(st, dec, (int)adv);
 }
 
 // Coefficients of a block are stored in zigzag (decode) order, int16 slots
@@ -321,7 +390,8 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
                                                     int16_t *__restrict__ dcv,
                                                     int32_t *__restrict__ status) {
   const int img = blockIdx.x;
-  if (status[img] != 0 || descs[img].nseg == 0) return;
+  // nseg 0: progressive (k_prog); sub_bits > 0: the parallel decoder
+  if (status[img] != 0 || descs[img].nseg == 0 || descs[img].sub_bits > 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
   const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, tid, 64);
@@ -344,8 +414,8 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
 }
 
 hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s) {
-  if (p.n == 0) return hipSuccess;
-  const size_t tab_lds = (size_t)(p.max_tabs < 1 ? 1 : p.max_tabs) * kTabU16 * 2;
+  if (p.n_serial == 0) return hipSuccess;
+  const size_t tab_lds = (size_t)huff_tab_lds(p.max_tabs);
   hipLaunchKernelGGL(k_huff_serial, dim3(p.n), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,
                      w.dstuf, w.coef, w.dcv, w.status);
   return hipGetLastError();
@@ -450,135 +520,40 @@ hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
 }
 
 // ===========================================================================
-// Parallel self-synchronising decode.
+// Parallel self-synchronising decode: one 1024-lane workgroup per image.
 //
-// A segment's bits are cut into subsequences of S bits; image-local slot lt
-// of segment s (sub_first <= lt < sub_first + sub_count) owns subsequence
-// j = lt - sub_first, i.e. bits [j*S, (j+1)*S). The decode state at a symbol
-// boundary is (p, b, k): bit position, block within the MCU, coefficient
-// index (k == 0: a DC symbol is next). A slot's exit state is the state at
-// the first symbol boundary p >= (j+1)*S; under its true entry state that is
-// its successor's true entry state. Two decoders in the same state decode
-// identically from there on — which is why chains started from a guessed
-// state converge (Huffman codes resynchronise).
+// A segment's bits are cut into subsequences of S bits; lane t of the image's
+// workgroup owns slot t, subsequence j = t - sub_first of the segment that
+// holds it, i.e. bits [j*S, (j+1)*S). The decode state at a symbol boundary is
+// (p, b, k): bit position, block within the MCU, coefficient index (k == 0: a
+// DC symbol is next). A slot's exit state is the state at the first symbol
+// boundary p >= (j+1)*S; under its true entry state that is its successor's
+// true entry state. Two decoders in the same state decode identically from
+// there on, which is why chains started from a guessed state converge (Huffman
+// codes resynchronise).
 //
-// Workgroup w = 256 lanes: lanes kHelpers..255 own slots
-// (w - wg_first) * kSlotsPerWg + lane - kHelpers; lanes 0..kHelpers-1 are
-// helpers that decode the kHelpers subsequences before the first slot, so its
-// entry state is right unless no chain resynchronised within kHelpers * S bits.
-// Inside the workgroup, lanes re-decode from their predecessor's exit until no
-// exit changes; each lane keeps two checkpoint states of its last trajectory
-// so a re-decode stops as soon as it merges with it. Across workgroups,
-// k_huff_fix compares the last helper's exit with the previous workgroup's
-// last exit and walks (one lane, LDS tables) only on a mismatch. The sync pass
-// only counts blocks per range; k_huff_write then decodes every range from its
-// true entry and k_dc_scan adds the DC predictors.
-//
-// LDS window: the workgroup's destuffed bytes, byte-swapped. Without
-// restart markers they span 256 * S/8 + 76 bytes; a workgroup whose ranges
-// span more (many small restart segments, kSegPad apart) reads global memory
-// instead. LDS per workgroup stays under a third of the CU's 160 KB at S = 1024
-// with four tables, so three decode workgroups share a CU.
+// The planner gives every image an S that fits all its slots in one workgroup
+// (S >= bits / (1024 - nseg)), so an image converges inside its workgroup:
+// no helper lanes, no walks across workgroup boundaries, and the block prefix
+// that places each range's coefficients is a workgroup scan. Per image:
+//   setup    the image's distinct tables and its whole destuffed stream
+//            (byte-swapped) into LDS; a stream larger than the window is read
+//            from global memory instead;
+//   phase 1  every lane decodes its range from a guessed state (b = 0, k = 0;
+//            exact at a segment start), counting blocks, and records its entry,
+//            exit and two checkpoints;
+//   rounds   a lane re-decodes only while its entry differs from its
+//            predecessor's exit; a re-decode stops at the first checkpoint
+//            where it merges with its own previous trajectory. The rounds end
+//            when no exit changed (at most one per slot: the true state only
+//            flows to the right);
+//   prefix   exclusive scan of the block counts: each range's first block;
+//   write    every lane decodes its range again from its true entry and stores
+//            coefficients (zigzag groups) and DC differences (k_dc_scan adds
+//            the predictors).
+// An image with more than kMaxParSegs restart segments takes k_huff_serial
+// instead: one lane per segment is already parallel there.
 // ===========================================================================
-
-__host__ __device__ inline int window_bytes(int S) { return 256 * (S / 8) + 128; }
-__host__ __device__ inline int window_lds_bytes(int S) {
-  const int words = window_bytes(S) / 4 + 1;
-  return (words * 4 + 15) & ~15;
-}
-
-// Locate the segment that owns image-local slot `lt` (sub_first ascending).
-__device__ __forceinline__ int find_segment(const Segment *__restrict__ segs, int seg_base, int nseg,
-                                            int lt) {
-  int lo = 0, hi = nseg - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (segs[seg_base + mid].sub_first <= lt) lo = mid;
-    else hi = mid - 1;
-  }
-  return seg_base + lo;
-}
-
-// Global state index of image-local slot lt.
-__device__ __forceinline__ int64_t slot_gt(const ImgDesc &d, int lt) {
-  return (int64_t)(d.wg_first + lt / kSlotsPerWg) * kSyncThreads + kHelpers + lt % kSlotsPerWg;
-}
-
-struct SubCtx {
-  int seg;        // segment index (global), -1 if idle
-  int j;          // subsequence index within the segment
-  int32_t seg_bits;
-  int32_t pbias;  // source bit of the segment's bit 0
-  bool active;    // a real slot
-  bool helper;    // a helper lane with a subsequence to decode
-  bool in_lds;    // the workgroup's window is in LDS (else global words)
-  const uint32_t *gw; // global words at the window base
-};
-
-// Workgroup setup shared by the sync and write kernels: the image's tables
-// and the LDS window.
-__device__ __forceinline__ Dec sub_setup(const ImgDesc &d, const Segment *__restrict__ segs,
-                                         const HuffTab *__restrict__ htabs, int S, int Smax,
-                                         const uint8_t *__restrict__ dstuf, lds_u32 win,
-                                         lds_u16 tabs, unsigned long long *sh_lohi, SubCtx &sc) {
-  const int tid = threadIdx.x;
-  const Dec dec = load_dec(d, htabs, tabs, tid, kSyncThreads);
-  const int lt0 = ((int)blockIdx.x - d.wg_first) * kSlotsPerWg;
-  const Segment &last = segs[d.seg_base + d.nseg - 1];
-  const int total_sub = last.sub_first + last.sub_count;
-  sc.active = false;
-  sc.helper = false;
-  sc.seg = -1;
-  sc.j = 0;
-  sc.seg_bits = 0;
-  sc.pbias = 0;
-  int64_t seg0 = 0;
-  uint64_t lo = ~0ull, hi = 0;
-  const int lt = tid >= kHelpers ? lt0 + tid - kHelpers : lt0;
-  if (lt < total_sub) {
-    const int si = find_segment(segs, d.seg_base, d.nseg, lt);
-    const Segment &sg = segs[si];
-    int j = lt - sg.sub_first;
-    if (tid >= kHelpers) {
-      sc.active = true;
-    } else {
-      j -= kHelpers - tid;
-      sc.helper = j >= 0;
-    }
-    if (sc.active || sc.helper) {
-      sc.seg = si;
-      sc.j = j;
-      seg0 = sg.byte_start;
-      sc.seg_bits = (int32_t)((sg.byte_end - sg.byte_start) * 8);
-      lo = (uint64_t)(sg.byte_start + ((int64_t)j * S) / 8);
-      int64_t h = sg.byte_start + ((int64_t)(j + 1) * S) / 8 + 64;
-      if (h > sg.byte_end + kSegPad) h = sg.byte_end + kSegPad;
-      hi = (uint64_t)h;
-    }
-  }
-  if (tid == 0) {
-    sh_lohi[0] = ~0ull;
-    sh_lohi[1] = 0;
-  }
-  __syncthreads();
-  if (hi > 0) {
-    atomicMin(&sh_lohi[0], (unsigned long long)lo);
-    atomicMax(&sh_lohi[1], (unsigned long long)hi);
-  }
-  __syncthreads();
-  int64_t wb = 0, nbytes = 0;
-  if (sh_lohi[1] > 0) {
-    wb = (int64_t)sh_lohi[0] & ~(int64_t)3;
-    nbytes = (((int64_t)sh_lohi[1] - wb) + 3) & ~(int64_t)3;
-  }
-  sc.in_lds = nbytes <= window_bytes(Smax);
-  sc.gw = reinterpret_cast<const uint32_t *>(dstuf + wb);
-  if (sc.in_lds)
-    for (int i = tid; i < (int)nbytes / 4; i += kSyncThreads) win[i] = __builtin_bswap32(sc.gw[i]);
-  sc.pbias = (int32_t)(seg0 - wb) * 8;
-  __syncthreads();
-  return dec;
-}
 
 // Checkpoints: the state at the first symbol boundary at/after
 // range_start + S/3 and + 2S/3, with the blocks counted up to it.
@@ -642,28 +617,64 @@ __device__ __forceinline__ bool count_run(Rd<W> &R, int32_t range_start, int32_t
   return false;
 }
 
-struct SyncLds {
-  int32_t ex_p[kSyncThreads];
-  uint16_t ex_bk[kSyncThreads]; // (3b << 8) | k <= 27 * 256 + 63
-  int any_changed;
+// Static LDS of k_huff_image (the window and the tables are dynamic).
+struct ImgLds {
+  int32_t ex_p[kHuffThreads];       // exit position (segment-relative); then the block prefix
+  uint16_t ex_bk[kHuffThreads];     // exit (3b << 8) | k <= 27 * 256 + 63
+  int32_t seg_first[kMaxParSegs + 1]; // sub_first of the image's segments; [nseg] = slots
+  int32_t scan[kHuffThreads / 64];
+  int32_t any_changed;
+  int32_t need_lanes, need_waves; // diagnostic counters (summed over rounds)
 };
+static_assert(sizeof(ImgLds) + 1024 <= kHuffStaticLds, "k_huff_image static LDS");
 
-// Phase 1 + intra-workgroup convergence for one lane; returns its block count.
-//
-// Phase 1 starts `warm` bits before the lane's range (never before its segment
-// or the window) from a guessed state (b = 0, k = 0), so the trajectory has
-// usually resynchronised by the range start; the lane records its entry state
-// (first symbol boundary at/after the range start) and its exit. A lane then
-// re-decodes only while its entry differs from its predecessor's exit, and a
-// re-decode stops at the first checkpoint where it merges with the lane's own
-// previous trajectory. The warm-up trades one extra range of decoding in phase
-// 1 for chains of wrong exits that are much rarer (they need a resync distance
-// above warm + S instead of S), which cuts the rounds of the slowest
-// workgroup, and with them the kernel's latency.
+// Exclusive prefix of v over the 1024-lane workgroup; contains __syncthreads.
+__device__ __forceinline__ int block_excl_scan1024(int v, int32_t *scratch, int *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int inc = wave_incl_scan(v);
+  if (lane == 63) scratch[wave] = inc;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kHuffThreads / 64; ++w) {
+    const int s = scratch[w];
+    base += w < wave ? s : 0;
+    tot += s;
+  }
+  *total = tot;
+  __syncthreads();
+  return base + inc - v;
+}
+
 template <class W>
-__device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec, int S, int warm,
-                                         SyncLds &sh, int32_t *__restrict__ dbg) {
+__device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
+                                             const Segment *__restrict__ segs, const Dec &dec,
+                                             int warm, uint64_t t_setup, ImgLds &sh,
+                                             int16_t *__restrict__ coef,
+                                             int16_t *__restrict__ dcv,
+                                             int32_t *__restrict__ status, int img,
+                                             int32_t *__restrict__ dbg) {
   const int tid = threadIdx.x;
+  const int S = d.sub_bits;
+  const bool live = tid < sh.seg_first[d.nseg];
+  int si = 0; // the lane's segment: last s with seg_first[s] <= tid
+  if (live) {
+    int lo = 0, hi = d.nseg - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sh.seg_first[mid] <= tid) lo = mid;
+      else hi = mid - 1;
+    }
+    si = lo;
+  }
+  const Segment &sg = segs[d.seg_base + si];
+  const int j = tid - sh.seg_first[si];
+  const int32_t pbias = (int32_t)(sg.byte_start - d.dst_off) * 8; // window word 0 = dst_off
+  const int32_t seg_bits = (int32_t)((sg.byte_end - sg.byte_start) * 8);
+  const int32_t rstart = pbias + j * S;
+  const int32_t stop = pbias + min((j + 1) * S, seg_bits);
+
+  // ---- phase 1: decode from a guess, optionally `warm` bits early ----
   int nblk = 0;
   Cp cp, none;
   cp.n = 0;
@@ -671,35 +682,45 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
   St st = make_state(0);
   Rd<W> R;
   R.src = src;
-  const int32_t rstart = sc.pbias + sc.j * S;
-  const int32_t stop = sc.pbias + min((sc.j + 1) * S, sc.seg_bits);
-  const bool live = sc.active || sc.helper;
-  int en_p = 0, en_bk = 0; // state at the range start (segment-relative position)
+  int en_p = 0, en_bk = 0; // entry state (segment-relative position)
   if (live) {
-    const int32_t w0 = max(rstart - warm, max(sc.pbias, 0));
+    const int32_t w0 = max(rstart - warm, pbias);
     R.seek(w0);
     if (w0 < rstart) {
       int skipped = 0;
       count_until(R, rstart, st, dec, skipped);
     }
-    en_p = R.p - sc.pbias;
+    en_p = R.p - pbias;
     en_bk = st.bk();
     count_run<false>(R, rstart, stop, S, st, dec, nblk, cp, none, 0);
-    sh.ex_p[tid] = R.p - sc.pbias;
+    sh.ex_p[tid] = R.p - pbias;
     sh.ex_bk[tid] = (uint16_t)st.bk();
   } else {
     sh.ex_p[tid] = 0;
     sh.ex_bk[tid] = 0;
   }
+
+  // ---- rounds: re-decode while the entry differs from the predecessor's exit ----
   int rounds = 0;
-  for (int round = 0; round < kSyncThreads + 1; ++round) {
+  uint64_t t_ph1 = 0;
+  for (int round = 0; round <= kHuffThreads; ++round) {
     ++rounds;
     __syncthreads();
-    if (tid == 0) sh.any_changed = 0;
+    if (tid == 0) {
+      sh.any_changed = 0;
+      if (round == 0) t_ph1 = wall_clock64();
+    }
     bool changed = false;
     int np = 0, nbk = 0;
-    const bool need = live && sc.j > 0 && tid > 0 &&
+    const bool need = live && j > 0 &&
                       (sh.ex_p[tid - 1] != en_p || sh.ex_bk[tid - 1] != en_bk);
+    {
+      const uint64_t bal = __ballot(need);
+      if ((tid & 63) == 0 && bal) {
+        atomicAdd(&sh.need_lanes, __popcll(bal));
+        atomicAdd(&sh.need_waves, 1);
+      }
+    }
     if (need) {
       en_p = sh.ex_p[tid - 1];
       en_bk = sh.ex_bk[tid - 1];
@@ -707,12 +728,12 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
       const int prev_total = nblk;
       const Cp prev = cp;
       nblk = 0;
-      R.seek(sc.pbias + en_p);
+      R.seek(pbias + en_p);
       if (count_run<true>(R, rstart, stop, S, st, dec, nblk, cp, prev, prev_total)) {
         np = sh.ex_p[tid];
         nbk = sh.ex_bk[tid];
       } else {
-        np = R.p - sc.pbias;
+        np = R.p - pbias;
         nbk = st.bk();
       }
       changed = (np != sh.ex_p[tid]) || (nbk != sh.ex_bk[tid]);
@@ -726,251 +747,119 @@ __device__ __forceinline__ int sync_lane(W src, const SubCtx &sc, const Dec &dec
     __syncthreads();
     if (!sh.any_changed) break;
   }
+  const uint64_t t_rounds = wall_clock64();
   if (dbg && tid == 0) {
     atomicAdd(dbg + 1, 1);
     atomicAdd(dbg + 2, rounds);
     atomicMax(dbg + 3, rounds);
   }
-  return nblk;
+
+  // ---- prefix of the block counts; the true entry is the predecessor's exit ----
+  int wp = 0, wbk = 0;
+  if (live && j > 0) {
+    wp = sh.ex_p[tid - 1];
+    wbk = sh.ex_bk[tid - 1];
+  }
+  // the write pass ends where the next range starts: this lane's exit (a
+  // count step may run past the range end); a segment's last range at its end
+  const int32_t wstop = j == sg.sub_count - 1 ? stop : pbias + sh.ex_p[tid];
+  int tot;
+  const int pre = block_excl_scan1024(live ? nblk : 0, sh.scan, &tot);
+  sh.ex_p[tid] = pre;
+  __syncthreads();
+  const uint64_t t_scan = wall_clock64();
+
+  // ---- write pass from the true entry ----
+  if (live) {
+    int cursor = pre - sh.ex_p[sh.seg_first[si]] - 1; // segment-relative block, -1 before the DC
+    const int total = sg.mcu_count * d.bpm;
+    const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
+    st = make_state(wbk);
+    R.seek(pbias + wp);
+    write_run(R, st, dec, wstop, cursor, total, coef + blk0 * 64, dcv + blk0);
+    if (j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
+  }
+  // diagnostic phase times (10 ns ticks summed over images; ldt_debug_counters)
+  __syncthreads();
+  if (dbg && tid == 0) {
+    const uint64_t t_end = wall_clock64();
+    atomicAdd(dbg + 9, (int)(t_ph1 - t_setup));
+    atomicAdd(dbg + 10, (int)(t_rounds - t_ph1));
+    atomicAdd(dbg + 11, (int)(t_scan - t_rounds));
+    atomicAdd(dbg + 12, (int)(t_end - t_scan));
+    atomicAdd(dbg + 13, sh.need_lanes);
+    atomicAdd(dbg + 14, sh.need_waves);
+  }
 }
 
-__global__ void __launch_bounds__(kSyncThreads) k_huff_sync(
+__global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
-    const int32_t *__restrict__ wg_img, int Smax, int warm_pct, SubState *__restrict__ sub,
-    const int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
-  __shared__ SyncLds sh;
-  __shared__ unsigned long long sh_lohi[2];
-  const int img = wg_img[blockIdx.x];
+    const int32_t *__restrict__ par_img, int win_bytes, int max_tabs, int warm_pct,
+    int16_t *__restrict__ coef,
+    int16_t *__restrict__ dcv, int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
+  __shared__ ImgLds sh;
+  const int img = par_img[blockIdx.x];
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
-  SubCtx sc;
-  const lds_u32 win = (lds_u32)dyn_lds;
-  const int S = d.sub_bits;
-  const Dec dec = sub_setup(d, segs, htabs, S, Smax, dstuf, win,
-                            (lds_u16)(dyn_lds + window_lds_bytes(Smax) / 4), sh_lohi, sc);
-  int nblk;
-  const int warm = (S * warm_pct) / 100;
-  if (sc.in_lds) nblk = sync_lane(LdsWords{(lds_cu32)win}, sc, dec, S, warm, sh, dbg);
-  else nblk = sync_lane(GlobWords{sc.gw}, sc, dec, S, warm, sh, dbg);
-  if (sc.active || tid == kHelpers - 1) {
-    SubState s;
-    s.exit_p = sh.ex_p[tid];
-    s.exit_bk = sh.ex_bk[tid];
-    s.nblk = nblk;
-    s.pad = 0;
-    sub[(int64_t)blockIdx.x * kSyncThreads + tid] = s;
+  const uint64_t t_start = wall_clock64();
+  // dynamic LDS: [window win_bytes][count tables][kTabU16 tables]
+  LDS_AS uint32_t *cnt = (LDS_AS uint32_t *)(dyn_lds + win_bytes / 4);
+  Dec dec = load_dec(d, htabs, (lds_u16)(cnt + (max_tabs << kLookBits)), tid, kHuffThreads);
+  dec.cnt = cnt;
+  for (int s = tid; s < d.nseg; s += kHuffThreads) sh.seg_first[s] = segs[d.seg_base + s].sub_first;
+  if (tid == 0) {
+    const Segment &l = segs[d.seg_base + d.nseg - 1];
+    sh.seg_first[d.nseg] = l.sub_first + l.sub_count;
+    sh.need_lanes = 0;
+    sh.need_waves = 0;
   }
-}
-
-// Lane 0 of the calling wave walks slots from lt0 (true entry = the stored
-// exit of slot lt0 - 1) until a recomputed exit equals the stored one. The
-// image's tables must already be in LDS (dec). bounded = true stops at the end
-// of lt0's workgroup and raises *redo (the next boundary then compared against
-// a stale exit).
-__device__ void boundary_walk(const ImgDesc &d, const Dec &dec, const Segment *__restrict__ segs,
-                              const uint8_t *__restrict__ dstuf, int S,
-                              SubState *__restrict__ sub, int lt0, bool bounded, int32_t *redo,
-                              int32_t *dbg) {
-  const int si = find_segment(segs, d.seg_base, d.nseg, lt0);
-  const Segment &sg = segs[si];
-  int j = lt0 - sg.sub_first;
-  if (j == 0) return;
-  const int32_t seg_bits = (int32_t)((sg.byte_end - sg.byte_start) * 8);
-  const SubState &pv = sub[slot_gt(d, lt0 - 1)];
-  int ep = pv.exit_p, ebk = pv.exit_bk;
-  int lt = lt0;
-  const int wg_next = (lt0 / kSlotsPerWg + 1) * kSlotsPerWg;
-  Rd<GlobWords> R;
-  R.src.w = reinterpret_cast<const uint32_t *>(dstuf + (sg.byte_start & ~(int64_t)3));
-  const int32_t pbias = (int32_t)(sg.byte_start & 3) * 8;
-  int steps = 0;
-  Cp cp, none;
-  none.n = 0;
-  while (true) {
-    ++steps;
-    St st = make_state(ebk);
-    int nblk = 0;
-    R.seek(pbias + ep);
-    count_run<false>(R, pbias + j * S, pbias + min((j + 1) * S, seg_bits), S, st, dec, nblk, cp,
-                     none, 0);
-    const int np = R.p - pbias, nbk = st.bk();
-    SubState &s = sub[slot_gt(d, lt)];
-    s.nblk = nblk;
-    if (np == s.exit_p && nbk == s.exit_bk) break; // converged
-    s.exit_p = np;
-    s.exit_bk = nbk;
-    ep = np;
-    ebk = nbk;
-    ++lt;
-    ++j;
-    if (j >= sg.sub_count) break; // end of segment: nothing downstream
-    if (bounded && lt >= wg_next) {
-      atomicExch(redo, 1);
-      if (dbg) atomicAdd(dbg + 7, 1);
-      break;
+  __syncthreads(); // kTabU16 tables in LDS
+  build_count_tables(dec, cnt, tid, kHuffThreads);
+  const int64_t need = destuff_region_bytes(d.src_len, d.nseg) + 16;
+  const bool in_lds = need <= win_bytes;
+  const uint8_t *base = dstuf + d.dst_off; // 16-aligned
+  if (in_lds) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u *g = reinterpret_cast<const v4u *>(base);
+    LDS_AS v4u *wl = (LDS_AS v4u *)dyn_lds;
+    for (int i = tid; i < (int)(need / 16); i += kHuffThreads) {
+      const v4u v = g[i];
+      v4u o;
+      o.x = __builtin_bswap32(v.x);
+      o.y = __builtin_bswap32(v.y);
+      o.z = __builtin_bswap32(v.z);
+      o.w = __builtin_bswap32(v.w);
+      wl[i] = o;
     }
   }
-  if (dbg) {
-    atomicAdd(dbg + 4, 1);
-    atomicAdd(dbg + 6, steps);
-    if (steps == 1) atomicAdd(dbg + 5, 1);
-  }
-}
-
-// One wave per decode workgroup: compare the last helper's candidate entry
-// for the workgroup's first slot with the true predecessor exit; walk on a
-// mismatch.
-__global__ void __launch_bounds__(64) k_huff_fix(const ImgDesc *__restrict__ descs,
-                                                 const Segment *__restrict__ segs,
-                                                 const HuffTab *__restrict__ htabs,
-                                                 const uint8_t *__restrict__ dstuf,
-                                                 const int32_t *__restrict__ wg_img, int Smax,
-                                                 SubState *__restrict__ sub,
-                                                 const int32_t *__restrict__ status,
-                                                 int32_t *__restrict__ redo) {
-  const int w = blockIdx.x;
-  const int img = wg_img[w];
-  if (status[img] != 0) return;
-  const ImgDesc &d = descs[img];
-  const int wl = w - d.wg_first;
-  const int lt0 = wl * kSlotsPerWg;
-  const Segment &last = segs[d.seg_base + d.nseg - 1];
-  if (wl == 0 || lt0 >= last.sub_first + last.sub_count) return;
-  const int si = find_segment(segs, d.seg_base, d.nseg, lt0);
-  if (lt0 == segs[si].sub_first) return; // the first slot starts a segment: exact entry
-  const SubState &pv = sub[slot_gt(d, lt0 - 1)];
-  const SubState &cand = sub[(int64_t)w * kSyncThreads + kHelpers - 1];
-  if (threadIdx.x == 0) atomicAdd(redo + 8, 1); // boundaries checked
-  if (pv.exit_p == cand.exit_p && pv.exit_bk == cand.exit_bk) return; // helpers were right
-  const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, threadIdx.x, 64);
   __syncthreads();
-  if (threadIdx.x == 0) boundary_walk(d, dec, segs, dstuf, d.sub_bits, sub, lt0, true, redo, redo);
-  (void)Smax;
-}
-
-// Fallback when a walk did not converge inside its workgroup: one lane per
-// image walks every workgroup boundary in order (always correct).
-__global__ void __launch_bounds__(64) k_huff_fix_serial(const ImgDesc *__restrict__ descs,
-                                                        const Segment *__restrict__ segs,
-                                                        const HuffTab *__restrict__ htabs,
-                                                        const uint8_t *__restrict__ dstuf, int Smax,
-                                                        SubState *__restrict__ sub,
-                                                        const int32_t *__restrict__ status,
-                                                        const int32_t *__restrict__ redo) {
-  const int img = blockIdx.x;
-  if (redo[0] == 0 || status[img] != 0 || descs[img].nseg == 0) return;
-  const ImgDesc &d = descs[img];
-  const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, threadIdx.x, 64);
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  const Segment &last = segs[d.seg_base + d.nseg - 1];
-  const int total = last.sub_first + last.sub_count;
-  for (int wl = 1; wl < d.wg_count; ++wl) {
-    const int lt0 = wl * kSlotsPerWg;
-    if (lt0 >= total) break;
-    boundary_walk(d, dec, segs, dstuf, d.sub_bits, sub, lt0, false, nullptr, nullptr);
-  }
-}
-
-// Exclusive prefix of nblk over each image's slots.
-__global__ void __launch_bounds__(256) k_huff_scan(const ImgDesc *__restrict__ descs,
-                                                   const Segment *__restrict__ segs,
-                                                   const SubState *__restrict__ sub,
-                                                   int32_t *__restrict__ pre,
-                                                   const int32_t *__restrict__ status) {
-  __shared__ int sh_scan[8];
-  const int img = blockIdx.x;
-  if (status[img] != 0 || descs[img].nseg == 0) return;
-  const ImgDesc &d = descs[img];
-  const Segment &last = segs[d.seg_base + d.nseg - 1];
-  const int total = last.sub_first + last.sub_count;
-  int run = 0;
-  for (int base = 0; base < total; base += 256) {
-    const int lt = base + threadIdx.x;
-    int v = 0;
-    int64_t gt = 0;
-    if (lt < total) {
-      gt = slot_gt(d, lt);
-      v = sub[gt].nblk;
-    }
-    int tot;
-    const int ex = block_excl_scan256(v, sh_scan, &tot);
-    if (lt < total) pre[gt] = run + ex;
-    run += tot;
-  }
-}
-
-template <class W>
-__device__ __forceinline__ void write_lane(W src, const SubCtx &sc, const Dec &dec, int S,
-                                           const ImgDesc &d, const Segment &sg, int entry, int bk,
-                                           int cursor, int16_t *__restrict__ coef,
-                                           int16_t *__restrict__ dcv,
-                                           int32_t *__restrict__ status, int img) {
-  St st = make_state(bk);
-  const int total = sg.mcu_count * d.bpm;
-  const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
-  Rd<W> R;
-  R.src = src;
-  R.seek(sc.pbias + entry);
-  write_run(R, st, dec, sc.pbias + min((sc.j + 1) * S, sc.seg_bits), cursor, total,
-            coef + blk0 * 64, dcv + blk0);
-  if (sc.j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
-}
-
-// Final pass: every slot decodes its range from its true entry state and
-// writes coefficients (DC differences to dcv).
-__global__ void __launch_bounds__(kSyncThreads) k_huff_write(
-    const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
-    const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
-    const int32_t *__restrict__ wg_img, int Smax, const SubState *__restrict__ sub,
-    const int32_t *__restrict__ pre, int16_t *__restrict__ coef,
-    int16_t *__restrict__ dcv, int32_t *__restrict__ status) {
-  __shared__ unsigned long long sh_lohi[2];
-  const int img = wg_img[blockIdx.x];
-  if (status[img] != 0) return;
-  const ImgDesc &d = descs[img];
-  const int tid = threadIdx.x;
-  SubCtx sc;
-  const lds_u32 win = (lds_u32)dyn_lds;
-  const int S = d.sub_bits;
-  const Dec dec = sub_setup(d, segs, htabs, S, Smax, dstuf, win,
-                            (lds_u16)(dyn_lds + window_lds_bytes(Smax) / 4), sh_lohi, sc);
-  if (!sc.active) return;
-  const Segment &sg = segs[sc.seg];
-  const int64_t gt = (int64_t)blockIdx.x * kSyncThreads + tid;
-  int entry = 0, bk = 0;
-  if (sc.j > 0) {
-    const int64_t pg = (tid == kHelpers) ? (int64_t)blockIdx.x * kSyncThreads - 1 : gt - 1;
-    const SubState &ps = sub[pg];
-    entry = ps.exit_p;
-    bk = ps.exit_bk;
-  }
-  const int cursor = pre[gt] - pre[slot_gt(d, sg.sub_first)] - 1;
-  if (sc.in_lds)
-    write_lane(LdsWords{(lds_cu32)win}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv,
-               status, img);
+  const uint64_t t_setup = wall_clock64();
+  if (dbg && tid == 0) atomicAdd(dbg + 8, (int)(t_setup - t_start));
+  const int warm = (d.sub_bits * warm_pct) / 100;
+  if (in_lds)
+    image_decode(LdsWords{(lds_cu32)dyn_lds}, d, segs, dec, warm, t_setup, sh, coef, dcv, status,
+                 img, dbg);
   else
-    write_lane(GlobWords{sc.gw}, sc, dec, S, d, sg, entry, bk, cursor, coef, dcv,
-               status, img);
+    image_decode(GlobWords{reinterpret_cast<const uint32_t *>(base)}, d, segs, dec, warm, t_setup,
+                 sh, coef, dcv, status, img, dbg);
 }
 
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {
-  if (p.n_wg == 0) return hipSuccess;
-  const size_t tab_lds = (size_t)(p.max_tabs < 1 ? 1 : p.max_tabs) * kTabU16 * 2;
-  const size_t dec_lds = (size_t)window_lds_bytes(p.subseq_bits) + tab_lds;
-  hipLaunchKernelGGL(k_huff_sync, dim3(p.n_wg), dim3(kSyncThreads), dec_lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.wg_img, p.subseq_bits, p.warm_pct, w.sub, w.status, p.redo);
-  hipLaunchKernelGGL(k_huff_fix, dim3(p.n_wg), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,
-                     w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.status, p.redo);
-  hipLaunchKernelGGL(k_huff_fix_serial, dim3(p.n), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,
-                     w.dstuf, p.subseq_bits, w.sub, w.status, p.redo);
-  hipLaunchKernelGGL(k_huff_scan, dim3(p.n), dim3(256), 0, s, p.descs, p.segs, w.sub, w.sub_pre,
-                     w.status);
-  hipLaunchKernelGGL(k_huff_write, dim3(p.n_wg), dim3(kSyncThreads), dec_lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.wg_img, p.subseq_bits, w.sub, w.sub_pre, w.coef,
-                     w.dcv, w.status);
+  if (p.n_par == 0) return hipSuccess;
+  static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_huff_image),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kHuffLdsMax - kHuffStaticLds);
+  if (getenv("LDT_DEBUG_LAUNCH"))
+    fprintf(stderr, "k_huff_image attr=%d n_par=%d win=%d tabs=%d static=%zu\n", (int)attr, p.n_par,
+            p.win_bytes, huff_tab_lds(p.max_tabs) + huff_cnt_lds(p.max_tabs), sizeof(ImgLds));
+  if (attr != hipSuccess) return attr;
+  const int tabs = p.max_tabs < 1 ? 1 : p.max_tabs;
+  const size_t lds = (size_t)p.win_bytes + huff_tab_lds(tabs) + huff_cnt_lds(tabs);
+  hipLaunchKernelGGL(k_huff_image, dim3(p.n_par), dim3(kHuffThreads), lds, s, p.descs, p.segs,
+                     p.htabs, w.dstuf, p.par_img, p.win_bytes, tabs, p.warm_pct, w.coef, w.dcv,
+                     w.status, p.redo);
   return hipGetLastError();
 }
 

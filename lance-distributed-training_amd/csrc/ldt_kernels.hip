@@ -260,8 +260,7 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
                                                         Segment *__restrict__ segs,
                                                         const int4 *__restrict__ cnt,
                                                         uint8_t *__restrict__ dst,
-                                                        int32_t *__restrict__ status,
-                                                        int subseq_bits) {
+                                                        int32_t *__restrict__ status) {
   __shared__ int sh_scan[8];
   __shared__ int sh_endc;
   const int img = blockIdx.x, tid = threadIdx.x;
@@ -302,11 +301,11 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
     if (rst_base != d.nseg - 1) segs[d.seg_base + s].byte_start = d.dst_off;
     segs[d.seg_base + s].byte_end = e;
   }
-  if (subseq_bits <= 0) return;
+  if (d.sub_bits <= 0) return; // serial Huffman decoder
   __syncthreads();
   // subsequence layout for the parallel Huffman decoder: segment s gets
-  // max(1, ceil(bits / S)) threads, numbered from 0 across the image, with the
-  // image's own S (the planner sizes it to fill whole workgroups).
+  // max(1, ceil(bits / S)) lanes, numbered from 0 across the image, with the
+  // image's own S (the planner sizes it so they fit one workgroup).
   const int S = d.sub_bits;
   int base = 0;
   for (int s0 = 0; s0 < d.nseg; s0 += 256) {
@@ -326,7 +325,7 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
     }
     base += tot;
   }
-  if (tid == 0 && base > d.sub_cap) status[img] = 3;
+  if (tid == 0 && base > kHuffThreads) status[img] = 3;
 }
 
 // ---------------------------------------------------------------------------
@@ -841,7 +840,7 @@ hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
                        p.chunk_img, w.ds_cnt, w.dstuf, w.status);
   }
   hipLaunchKernelGGL(k_destuff_layout, dim3(p.n), dim3(256), 0, s, p.descs, p.segs, w.ds_cnt,
-                     w.dstuf, w.status, p.subseq_bits);
+                     w.dstuf, w.status);
   return hipGetLastError();
 }
 

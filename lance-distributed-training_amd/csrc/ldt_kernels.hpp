@@ -29,13 +29,14 @@ struct DevPlan {
   int n, nseg;
   int max_ks_h, max_ks_v, max_w, max_h;
   int64_t max_blocks;
-  // parallel Huffman decode
-  int subseq_bits;
-  int warm_pct;          // sync phase-1 warm-up before each range, % of S
-  int n_wg;              // total subsequence workgroups
-  const int32_t *wg_img; // workgroup -> image
-  int32_t *redo;         // set when a workgroup-boundary walk did not converge
-  int max_tabs;          // max distinct Huffman tables of one image (LDS slots)
+  // Huffman decode: k_huff_image (one workgroup per image) and k_huff_serial
+  int n_par;              // images on the parallel decoder
+  const int32_t *par_img; // its workgroup -> image
+  int n_serial;           // images on the serial decoder (sub_bits == 0)
+  int win_bytes;          // LDS window of k_huff_image (images needing more read global memory)
+  int warm_pct;           // phase-1 warm-up before each range, % of S
+  int32_t *redo;          // debug counters of the parallel decoder (16 ints)
+  int max_tabs;           // max distinct Huffman tables of one image (LDS slots)
   int n_fast420;         // images on k_resize4's fast staging path (resize_fast420)
   // progressive images (k_prog, one workgroup each)
   int n_prog;
@@ -55,8 +56,6 @@ struct DevWork {
   int16_t *dcv;         // per block: DC difference (Huffman), then absolute DC (k_dc_scan)
   uint8_t *planes;      // component planes
   int32_t *status;      // per image
-  SubState *sub;        // per subsequence thread (n_wg * 256)
-  int32_t *sub_pre;     // exclusive prefix of nblk per thread
   int4 *ds_cnt;         // per destuff chunk: kept bytes, RSTn markers, end marker seen
 };
 

@@ -35,13 +35,12 @@ struct ImgDesc {
   int32_t dct[3], act[3];  // Huffman table indices (plan table array)
   uint8_t bcomp[kMaxBlocksPerMcu], bdx[kMaxBlocksPerMcu], bdy[kMaxBlocksPerMcu];
   uint8_t pad_[2];
-  // parallel Huffman decode: this image's subsequence threads occupy
-  // workgroups [wg_first, wg_first + wg_count) (256 threads each)
-  int32_t wg_first, wg_count;
-  int32_t sub_cap;   // thread slots reserved (>= sum of segment sub_count)
   // destuff: this image's 4 KB chunks are [ds_first, ds_first + ds_count)
   int32_t ds_first, ds_count;
-  int32_t sub_bits;  // parallel Huffman subsequence length S of this image (bits)
+  // parallel Huffman decode (k_huff_image, one workgroup per image): the
+  // subsequence length S of this image in bits; 0 = the serial decoder
+  int32_t sub_bits;
+  int32_t pad1_;
   // progressive (SOF2) images: scans [prog_first, prog_first + prog_count) of
   // the plan's scan table, decoded by k_prog; nseg == 0 (no baseline segments)
   int32_t prog_first, prog_count;
@@ -68,25 +67,22 @@ struct Segment {
   int32_t pad_[3];
 };
 
-// Per-subsequence-thread decode state of the parallel Huffman decoder.
-struct SubState {
-  int32_t exit_p;   // bit position (segment-relative) of the first symbol at/after the range end
-  int32_t exit_bk;  // (3 * b << 8) | k at that symbol (b: block within the MCU)
-  int32_t nblk;     // DC symbols decoded inside the range (blocks started)
-  int32_t pad;
-};
-
-constexpr int kSyncThreads = 256;
-// Lanes 0..kHelpers-1 of every decode workgroup are helpers: they decode the
-// kHelpers subsequences just before the workgroup's first slot, so the first
-// slot's entry state is almost always right before any cross-workgroup fix.
-// Lanes kHelpers..255 own subsequence slots.
-constexpr int kHelpers = 8;
-constexpr int kSlotsPerWg = kSyncThreads - kHelpers;
+// Parallel Huffman decoder (k_huff_image): one workgroup of kHuffThreads
+// lanes per image, one subsequence slot per lane. Images with more restart
+// segments than kMaxParSegs take the serial decoder (one lane per segment).
+constexpr int kHuffThreads = 1024;
+constexpr int kMaxParSegs = 512;
+constexpr int kHuffLdsMax = 160 * 1024;   // LDS per CU (gfx950)
+constexpr int kHuffStaticLds = 10 * 1024; // k_huff_image's static LDS (ImgLds) + margin
 // Zero bytes after every destuffed segment (restart interval): a bit reader
 // may look up to 8 bytes past a segment without a bounds check and reads the
 // zeros libjpeg inserts at a marker (jdhuff.c jpeg_fill_bit_buffer).
 constexpr int kSegPad = 8;
+// Destuffed bytes reserved for an image (all segments, their pads, slack);
+// 16-aligned, so every image's region starts 16-aligned.
+__host__ __device__ inline int64_t destuff_region_bytes(int64_t src_len, int nseg) {
+  return (src_len + 16 + (int64_t)kSegPad * nseg + 15) & ~(int64_t)15;
+}
 // Destuff work unit: bytes of entropy-coded data per workgroup.
 constexpr int kDsChunkBytes = 4096;
 
@@ -105,6 +101,14 @@ constexpr int kL2Chunks = 8;
 constexpr int kL2Bits = 16 - kLookBits;
 constexpr int kTabU16 = (1 << kLookBits) + (kL2Chunks << kL2Bits); // uint16 entries per table
 constexpr uint32_t kHuffCanon = 15u << 5;
+// LDS bytes of an image's distinct Huffman tables in the decoders
+__host__ __device__ inline int huff_tab_lds(int max_tabs) {
+  return (max_tabs < 1 ? 1 : max_tabs) * kTabU16 * 2;
+}
+// ... and of the parallel decoder's count-mode tables (uint32, 2^kLookBits each)
+__host__ __device__ inline int huff_cnt_lds(int max_tabs) {
+  return (max_tabs < 1 ? 1 : max_tabs) * (4 << kLookBits);
+}
 __host__ __device__ inline uint16_t huff_entry(int len, int sym, bool dc) {
   int s, adv;
   if (dc) {

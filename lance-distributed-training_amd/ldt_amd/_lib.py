@@ -42,7 +42,6 @@ OPT_HUFF_MODE = 2
 OPT_SUBSEQ_BITS = 3
 OPT_PROFILE = 4
 OPT_RESIZE_IMPL = 5
-OPT_SUBSEQ_FIT = 6
 OPT_SYNC_WARM = 7
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")

@@ -269,10 +269,11 @@ def test_lance_dataset_end_to_end(tmp_path):
         _check(first["image"][k].cpu().numpy(), oracle.jpeg_to_tensor(cells[k]), f"loader[{k}]")
 
 
-@pytest.mark.parametrize("mode,bits", [(1, 1024), (2, 64), (2, 256), (2, 1024), (2, 2048)])
+@pytest.mark.parametrize("mode,bits", [(1, 1024), (2, 64), (2, 256), (2, 1024), (2, 4096)])
 def test_huffman_decoder_modes(mode, bits, manifest):
-    """Serial-per-segment and parallel self-synchronising decoders (with small
-    subsequences that force many workgroup-boundary walks) agree bit-exactly."""
+    """Serial-per-segment and parallel self-synchronising decoders agree
+    bit-exactly; the minimum subsequence length ranges from 64 bits (many
+    convergence rounds on the small golden images) to 4096."""
     import torch
 
     import ldt_amd
@@ -295,7 +296,23 @@ def test_huffman_decoder_modes(mode, bits, manifest):
         assert ei.value.rows == {1: 3}
     finally:
         ctx.set_option(_lib.OPT_HUFF_MODE, 0)
-        ctx.set_option(_lib.OPT_SUBSEQ_BITS, 1024)
+        ctx.set_option(_lib.OPT_SUBSEQ_BITS, 256)
+
+
+def test_many_restart_segments_take_serial_decoder():
+    """An image with more than 512 restart segments (a marker every MCU) goes
+    to the serial decoder while its batch-mates use the per-image parallel
+    decoder; both bit-exact vs the oracle in one batch."""
+    import ldt_amd
+    from ldt_amd import synth
+
+    many = synth.encode(synth.field(512, 512, 91, 6.0), quality=90, restart_marker_blocks=1)
+    few = synth.encode(synth.field(384, 512, 92, 6.0), quality=90, restart_marker_rows=1)
+    c2, _ = synth.q90_512(2, seed=93)
+    cells = [c2[0], many, few, c2[1]]
+    out = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+    for k, b in enumerate(cells):
+        _check(out[k], oracle.jpeg_to_tensor(b), f"restart-mix[{k}]")
 
 
 def test_large_image_streaming_fallback_and_too_large():

@@ -1,0 +1,28 @@
+"""Diagnostic: parallel Huffman sync counters (rounds per workgroup, boundary
+walks) for the c2/c1/c4 workloads at the default subsequence length."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "lance-distributed-training_amd"))
+import ldt_amd  # noqa: E402
+from ldt_amd import _lib, synth  # noqa: E402
+
+ctx = _lib.get_context(0)
+names = ["redo", "wgs", "rounds_sum", "rounds_max", "walks", "walk_first", "walk_steps", "fallbacks",
+         "t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "need_lanes", "need_waves"]
+for wl, fn, n in (("c2", synth.q90_512, 256), ("c1", synth.food101_like, 128), ("c4", synth.imagenet_like, 128)):
+    cells, labels = fn(n, seed=1000)
+    rb = ldt_amd.ResidentBatch(cells, labels)
+    rb.decode()
+    out = np.zeros(16, np.int32)
+    ctx.check(ctx.lib.ldt_debug_counters(ctx.handle, out.ctypes.data, None), "dbg")
+    d = dict(zip(names, out[:15].tolist()))
+    w = max(d["wgs"], 1)
+    d["rounds_avg"] = round(d["rounds_sum"] / w, 2)
+    for k in ("t_setup", "t_phase1", "t_rounds", "t_scan", "t_write"):
+        d[k + "_us"] = round(d.pop(k) / w / 100.0, 2)  # 10 ns ticks per image
+    d["need_lanes_per_round"] = round(d["need_lanes"] / max(d["rounds_sum"], 1), 1)
+    d["need_waves_per_round"] = round(d["need_waves"] / max(d["rounds_sum"], 1), 2)
+    print(wl, d, flush=True)
