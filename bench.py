@@ -10,9 +10,11 @@ configs[1] — 512x512 baseline JPEG, 4:2:0, q90, batch 256 per GPU.
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line. The CPU baseline (rank 0, N=1 only) times the
-reference recipe — Pillow open/convert/resize(BILINEAR) + to_tensor, i.e.
-lance_map_style.py:21-44's collate_fn — over a bounded sample with 8 worker
-processes (the reference's num_workers default, lance_map_style.py:137).
+reference's own CPU path on this host in this run: the map-style DataLoader
+harness with the PIL collate_fn (lance_map_style.py:21-44, :54-69) at
+num_workers 8 and at the box's CPU share, and the iterable to_tensor_fn in
+one process (cpu_baseline below). value_host_input is the PCIe-inclusive rate
+of the same steps (host RecordBatches).
 """
 from __future__ import annotations
 
@@ -57,41 +59,91 @@ def make_cells(workload: str, n: int, seed: int):
     raise ValueError(workload)
 
 
-def cpu_baseline(cells, workers: int = 8, target_images: int = 3072):
-    """Reference CPU recipe on a bounded sample: PIL decode/resize + to_tensor
-    via a spawn pool of `workers` processes (DataLoader num_workers=8)."""
-    import multiprocessing as mp
+CPU_SHARE = 16  # CPUs of the GPU box a run may use per GPU (os.cpu_count() shows the whole host)
+
+
+def _rates(times, imgs):
+    r = sorted(imgs / t for t in times)
+    return {"best": round(r[-1], 1), "median": round(r[len(r) // 2], 1), "reps": [round(x, 1) for x in r]}
+
+
+def cpu_baseline(cells, labels, batch: int = 128, reps: int = 3):
+    """The reference's CPU path on this host, in this run.
+
+    map-style legs: lance_map_style.py:54-69's harness, i.e. a stock torch
+    DataLoader over the SafeLanceDataset shim with the reference PIL collate_fn
+    (oracle.pil_collate_fn = lance_map_style.py:21-44: Pillow
+    open/convert/Resize((224,224))/to_tensor, stack), batch 128 (config 1),
+    pin_memory=True, persistent spawn workers; num_workers = 8 (the reference
+    default, :137) and the box's CPU share. Each leg: one batch per worker
+    (plus the prefetch queue) to warm up, then `reps` timed runs of
+    num_workers batches; best and median img/s.
+    iterable leg: lance_iterable.py:38-50's decode_tensor_image on
+    RecordBatches in the main process (num_workers=0, :75-77)."""
+    import importlib
+    import shutil
+    import tempfile
 
     import numpy as np
+    import pyarrow as pa
+    import torch
+    from PIL import __version__ as pil_version
     from PIL import features
 
     from oracle import oracle
 
-    sample = [cells[i % len(cells)] for i in range(target_images)]
-    ctx = mp.get_context("spawn")
-    with ctx.Pool(workers) as pool:
-        pool.map(oracle.pil_image_to_tensor, sample[: workers * 4], chunksize=1)  # warm workers
-        t0 = time.perf_counter()
-        for _ in pool.imap_unordered(oracle.pil_image_to_tensor, sample, chunksize=16):
-            pass
-        dt = time.perf_counter() - t0
-    # iterable path: one process, num_workers=0 (lance_iterable.py:75-77)
-    one = sample[:128]
-    t1 = time.perf_counter()
-    for b in one:
-        oracle.pil_image_to_tensor(b)
-    dt1 = time.perf_counter() - t1
-    import PIL
-
+    lds = importlib.import_module("ldt_amd.dataset")  # the package exports a dataset() function
+    tmp = tempfile.mkdtemp(prefix="ldt_cpu_")
+    try:
+        n = len(cells)
+        lds.write_dataset(pa.table({"image": pa.array(cells, pa.binary()),
+                                    "label": pa.array(np.asarray(labels, np.int64))}), tmp)
+        ds = lds.SafeLanceDataset(tmp)
+        host = len(os.sched_getaffinity(0))
+        legs = []
+        for w in sorted({8, min(host, CPU_SHARE)}):
+            need = batch * w * (2 + 2 + reps)  # warm-up + prefetch queue + timed
+            order = [i % n for i in range(need)]
+            loader = lds.get_safe_loader(ds, batch_size=batch, sampler=order, num_workers=w,
+                                         collate_fn=oracle.pil_collate_fn, pin_memory=True,
+                                         persistent_workers=True)
+            it = iter(loader)
+            for _ in range(4 * w):  # every worker busy, prefetch queues full
+                next(it)
+            times = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                for _ in range(w):
+                    out = next(it)
+                times.append(time.perf_counter() - t0)
+            assert out["image"].shape == (batch, 3, 224, 224)
+            del it, loader
+            legs.append(dict(harness="map-style DataLoader(SafeLanceDataset, PIL collate_fn)",
+                             num_workers=w, batch=batch, **_rates(times, batch * w)))
+        rb = pa.RecordBatch.from_arrays([pa.array(cells[:batch], pa.binary()),
+                                         pa.array(np.asarray(labels[:batch], np.int64))],
+                                        names=["image", "label"])
+        oracle.pil_decode_tensor_image(rb)
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            oracle.pil_decode_tensor_image(rb)
+            times.append(time.perf_counter() - t0)
+        legs.append(dict(harness="iterable decode_tensor_image in the main process", num_workers=0,
+                         batch=batch, **_rates(times, batch)))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    ref = legs[0]
     return {
-        "value": round(target_images / dt, 1), "unit": "img/s", "cores": workers, "kind": "reference",
-        "sample": (f"{target_images} images of this workload through the reference recipe "
-                   f"(Pillow {PIL.__version__}/libjpeg-turbo {features.version_feature('libjpeg_turbo')} "
-                   f"open->convert(RGB)->resize((224,224),BILINEAR)->to_tensor) in a spawn pool of "
-                   f"{workers} processes (map-style num_workers=8, lance_map_style.py:137); "
-                   f"host affinity {len(os.sched_getaffinity(0))} cpus"),
-        "iterable_1proc_img_s": round(len(one) / dt1, 1),
-        "cpu_work_s": round(dt * workers, 1),
+        "value": ref["median"], "unit": "img/s", "cores": ref["num_workers"], "kind": "reference",
+        "sample": (f"the reference CPU path on this workload's cells: DataLoader(SafeLanceDataset shim, "
+                   f"PIL collate_fn, batch {batch}, pin_memory, persistent spawn workers), "
+                   f"{reps} x num_workers timed batches per leg after warm-up; Pillow {pil_version} / "
+                   f"libjpeg-turbo {features.version_feature('libjpeg_turbo')}; host affinity {host} CPUs "
+                   f"(a one-GPU run may use {CPU_SHARE}); value = median of the "
+                   f"num_workers={ref['num_workers']} leg (lance_map_style.py:137 default)"),
+        "legs": legs,
+        "torch_threads": torch.get_num_threads(),
     }
 
 
@@ -103,7 +155,6 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-images", type=int, default=3072)
     ap.add_argument("--input", choices=("resident", "host"), default="resident",
                     help="resident: cells already in HBM (value); host: Arrow RecordBatches in host "
                          "memory through the pipelined to_tensor_fn (PCIe-inclusive, DESIGN.md §7)")
@@ -153,18 +204,20 @@ def main():
         def step():
             return ldt_amd.resize_raw(raw, 1024, 1024, normalize=True)
     else:
-        nb = 2  # two distinct resident batches, alternated
-        batches = []
-        cells_all = []
+        nb = 2  # two distinct batches, alternated
+        batches, host_batches = [], []
+        cells_all, labels_all = [], []
         import pyarrow as pa
 
         for k in range(nb):
             cells, labels = make_cells(args.workload, B, seed=1000 * rank + k)
             cells_all += cells
+            labels_all += list(labels)
+            host_batches.append(pa.RecordBatch.from_arrays(
+                [pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
+                names=["image", "label"]))
             if args.input == "host":
-                batches.append(pa.RecordBatch.from_arrays(
-                    [pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
-                    names=["image", "label"]))
+                batches.append(host_batches[-1])
             else:
                 batches.append(ldt_amd.ResidentBatch(cells, labels, device=dev))
         px = [ldt_amd_dims(c) for c in cells_all[:B]]
@@ -208,6 +261,25 @@ def main():
     elapsed_max = float(t.item())
     total_imgs = B * args.steps * world
     value = total_imgs / elapsed_max
+
+    # PCIe-inclusive rate in the same run: the same steps with
+    # the cells in host Arrow RecordBatches through the pipelined to_tensor_fn
+    value_host = None
+    if args.workload != "c5" and args.input == "resident":
+        hp = ldt_amd.DecodePipeline(depth=args.depth, device=dev)
+        for k in range(max(args.warmup, 2)):
+            hp.decode(host_batches[k % nb])
+        barrier()
+        th0 = time.perf_counter()
+        for k in range(args.steps):
+            hp.decode(host_batches[k % nb])
+        barrier()
+        th = torch.tensor([time.perf_counter() - th0], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(th, op=dist.ReduceOp.MAX)
+        hp.check()
+        value_host = B * args.steps * world / float(th.item())
 
     # standalone launch durations (one batch in flight, after the timed region)
     standalone = None
@@ -282,9 +354,14 @@ def main():
         res["decode_efficiency"] = dec
     if args.workload != "c5":
         res["config"]["compressed_bytes_per_img"] = round(comp_bytes, 1)
+    if value_host is not None:
+        res["value_host_input"] = round(value_host, 1)
+        res["value_host_input_note"] = ("same steps with the cells in host pa.RecordBatches (pinned copy + "
+                                        "H2D every step, to_tensor_fn boundary); value keeps them in HBM")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "c5":
-        res["cpu_baseline"] = cpu_baseline(cells_all[:B], workers=8, target_images=args.cpu_images)
-        res["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 2)
+        res["cpu_baseline"] = cpu_baseline(cells_all, labels_all)
+        res["gpu_over_cpu"] = {f"num_workers={leg['num_workers']}": round(value / leg["median"], 1)
+                               for leg in res["cpu_baseline"]["legs"]}
     elif rank == 0 and world == 1 and args.workload == "c5" and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_raw(raw[:8].cpu().numpy())
         res["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 2)

@@ -58,7 +58,7 @@ extern "C" {
                                  later with ldt_fetch_status()                  */
 #define LDT_OPT_HUFF_MODE 2   /* 0 auto (default) and 2: the parallel
                                  self-synchronising decoder, one workgroup per
-                                 image (the serial one for images with > 512
+                                 image (the serial one for images with > 256
                                  restart segments); 1: serial per segment      */
 #define LDT_OPT_SUBSEQ_BITS 3 /* minimum subsequence length of the parallel
                                  decoder: 64..8192 bits, multiple of 32

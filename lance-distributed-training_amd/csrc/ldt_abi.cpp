@@ -567,7 +567,9 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     }
     d.src_off = ip.cell_off + H.scan_pos;
     d.src_len = ip.cell_len - H.scan_pos;
-    if (parallel && d.nseg <= kMaxParSegs) {
+    const int64_t par_room = kHuffThreads - (int64_t)d.nseg;
+    const int64_t par_s = (d.src_len * 8 + par_room - 1) / std::max<int64_t>(par_room, 1);
+    if (parallel && d.nseg <= kMaxParSegs && par_s <= kMaxParS - 64) {
       // k_huff_image: all of the image's slots in one workgroup. Slots are
       // sum over segments of ceil(bits_s / S) <= bits / S + nseg, so
       // S >= bits / (kHuffThreads - nseg) fits; the option is a lower bound.
@@ -669,7 +671,9 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
 
   // ---- device workspace ----
   if ((rc = ensure_dev(c, c->d_plan, (size_t)plan_bytes, s))) return rc;
-  if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 64, s))) return rc;
+  // slack: a decoder finishing its last block may read a few hundred bytes
+  // past an image's region
+  if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 1024, s))) return rc;
   // coefficients: all zero between batches (k_idct clears every block it
   // reads), so they are zeroed only when allocated
   if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 128 + 64, s, true))) return rc;
@@ -712,8 +716,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   {
     // LDS window of k_huff_image: the largest image's stream, capped by what
     // is left of the CU's LDS after the tables (bigger streams read global)
-    const int64_t cap =
-        kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs) - huff_cnt_lds(max_tabs);
+    const int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs);
     p.win_bytes = (int)(std::min<int64_t>(max_window, cap) & ~(int64_t)15);
   }
   p.warm_pct = c->warm_pct;

@@ -112,8 +112,7 @@ struct Rd {
 // (b3, k): 3 * (block within the MCU) and the coefficient index (0: DC next).
 // ---------------------------------------------------------------------------
 struct Dec {
-  lds_cu16 tabs;     // the image's distinct tables, kTabU16 entries per slot
-  const LDS_AS uint32_t *cnt; // count-mode tables, 2^kLookBits entries per slot (k_huff_image)
+  lds_cu16 tabs;     // the image's distinct tables, kTabStride uint16 per slot
   uint32_t dcseq;    // LDS table slot of MCU block b's DC table at bits 3b
   uint32_t acseq;    // ... AC table
   int b3end;         // 3 * blocks per MCU
@@ -162,18 +161,17 @@ __device__ __forceinline__ Dec load_dec(const ImgDesc &d, const HuffTab *__restr
   int slot_tab[6];
   uint32_t slotmap;
   const int ns = image_slots(d, slotmap, slot_tab);
-  constexpr int kWords = kTabU16 / 2;
+  constexpr int kWords = kTabStride / 2;
   for (int i = tid; i < ns * kWords; i += nthreads) {
     const int q = i / kWords, o = i - q * kWords;
     int tix = slot_tab[0];
 #pragma unroll
     for (int x = 1; x < 6; ++x)
       if (q == x) tix = slot_tab[x];
-    ((LDS_AS uint32_t *)(tabs + q * kTabU16))[o] = reinterpret_cast<const uint32_t *>(htabs + tix)[o];
+    ((LDS_AS uint32_t *)(tabs + q * kTabStride))[o] = reinterpret_cast<const uint32_t *>(htabs + tix)[o];
   }
   Dec dec;
   dec.tabs = tabs;
-  dec.cnt = nullptr;
   dec.dcseq = dec.acseq = 0;
   for (int b = 0; b < d.bpm; ++b) {
     const int c = d.bcomp[b] & 3;
@@ -208,11 +206,11 @@ __device__ __attribute__((noinline)) uint32_t lookup_canon(const HuffTab *__rest
 __device__ __forceinline__ uint32_t lookup(const Dec &dec, const St &st, uint32_t pk) {
   const bool ac = st.k != 0;
   const uint32_t slot = __builtin_amdgcn_ubfe(ac ? dec.acseq : dec.dcseq, (uint32_t)st.b3, 3u);
-  const lds_cu16 t = dec.tabs + slot * kTabU16;
-  uint32_t e = t[pk >> (32 - kLookBits)];
+  const lds_cu16 t = dec.tabs + slot * kTabStride;
+  uint32_t e = ((const LDS_AS uint32_t *)t)[pk >> (32 - kLookBits)] & 0xFFFFu;
   if (__builtin_expect((e & 31) == 0, 0)) {
     if (e != kHuffCanon)
-      e = t[(1 << kLookBits) + ((e >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
+      e = t[kL2Off + ((e >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
     else
       e = lookup_canon(dec.g, dec.d, st.b3 / 3, ac, pk);
   }
@@ -237,69 +235,29 @@ __device__ __forceinline__ void advance(St &st, const Dec &dec, int adv) {
   st.k = end ? 0 : k2;
 }
 
-// Count-mode tables (k_huff_image's sync passes only count blocks, so one
-// lookup may consume several symbols). Entry for each kLookBits-bit peek:
-//   T (bits 0-4)     bits of the longest run of AC symbols of one block whose
-//                    codes all lie in the peeked bits (the last symbol's
-//                    magnitude may extend past them)
-//   ADV (5-11)       coefficient advance of the whole run (EOB 64 ends it)
-//   PRE (12-18)      advance before the run's last symbol: the run is valid
-//                    only if k + PRE < 64 (no block ends inside it)
-//   t1, adv1 (19-23, 24-30)  the first symbol alone
-// DC tables hold single symbols. T == 0: a long code, the entry is the kTabU16
-// table's indirect entry (second level / canonical search).
-__device__ __forceinline__ void build_count_tables(const Dec &dec, LDS_AS uint32_t *cnt, int tid,
-                                                   int nthreads) {
-  constexpr uint32_t kMask = (1u << kLookBits) - 1;
-  for (int i = tid; i < (dec.ns << kLookBits); i += nthreads) {
-    const int q = i >> kLookBits;
-    const uint32_t x = (uint32_t)i & kMask;
-    const lds_cu16 tb = dec.tabs + q * kTabU16;
-    const uint32_t e = tb[x];
-    const uint32_t t1 = e & 31;
-    uint32_t c = e; // indirect: as the kTabU16 entry
-    if (t1 != 0) {
-      const uint32_t adv1 = e >> 9;
-      uint32_t T = t1, ADV = adv1, PRE = 0;
-      if ((dec.acmask >> q) & 1) {
-        while (ADV < 64 && T < (uint32_t)kLookBits) {
-          const uint32_t e2 = tb[(x << T) & kMask];
-          const uint32_t t2 = e2 & 31;
-          if (t2 == 0) break;
-          const uint32_t cl2 = t2 - ((e2 >> 5) & 15); // code length
-          if (T + cl2 > (uint32_t)kLookBits || ADV >= 63) break;
-          PRE = ADV;
-          ADV += e2 >> 9;
-          T += t2;
-        }
-      }
-      c = T | (ADV << 5) | (PRE << 12) | (t1 << 19) | (adv1 << 24);
-    }
-    cnt[i] = c;
-  }
-}
-
-// Count-only step (blocks started): one count-table lookup, one or more symbols.
+// Count-only step (blocks started) on the count-mode entries (HuffTab.cnt,
+// see ldt_types.hpp): one lookup consumes a run of AC symbols of one block
+// when k + PRE < 64, else the first symbol alone.
 template <class W>
 __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int &nblk) {
   const uint32_t pk = R.peek();
   const bool ac = st.k != 0;
   const uint32_t slot = __builtin_amdgcn_ubfe(ac ? dec.acseq : dec.dcseq, (uint32_t)st.b3, 3u);
-  const uint32_t c = dec.cnt[(slot << kLookBits) + (pk >> (32 - kLookBits))];
-  uint32_t t, adv;
-  if (__builtin_expect((c & 31) == 0, 0)) {
-    const lds_cu16 tb = dec.tabs + slot * kTabU16;
+  const lds_cu16 tb = dec.tabs + slot * kTabStride;
+  const uint32_t w = ((const LDS_AS uint32_t *)tb)[pk >> (32 - kLookBits)];
+  const uint32_t c = w >> 16, e1 = w & 0xFFFFu;
+  // the run, or its first symbol alone when a block would end inside it
+  const bool ok = (uint32_t)st.k + (c >> 12) < 64;
+  uint32_t t = ok ? (c & 31) : (e1 & 31);
+  uint32_t adv = ok ? ((c >> 5) & 127) : (e1 >> 9);
+  if (__builtin_expect((e1 & 31) == 0, 0)) { // long code
     uint32_t e;
-    if (c != kHuffCanon)
-      e = tb[(1 << kLookBits) + ((c >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
+    if (e1 != kHuffCanon)
+      e = tb[kL2Off + ((e1 >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
     else
       e = lookup_canon(dec.g, dec.d, st.b3 / 3, ac, pk);
     t = e & 31;
     adv = e >> 9;
-  } else {
-    const bool ok = (uint32_t)st.k + ((c >> 12) & 127) < 64;
-    t = ok ? (c & 31) : ((c >> 19) & 31);
-    adv = ok ? ((c >> 5) & 127) : (c >> 24);
   }
   nblk += st.k == 0 ? 1 : 0;
   R.consume((int)t);
@@ -617,16 +575,27 @@ __device__ __forceinline__ bool count_run(Rd<W> &R, int32_t range_start, int32_t
   return false;
 }
 
-// Static LDS of k_huff_image (the window and the tables are dynamic).
+// Static LDS of k_huff_image (the window and the tables are dynamic): the
+// decode state of every slot, so that a round's re-decodes can be packed into
+// the first waves of the workgroup (any lane may work on any slot).
 struct ImgLds {
-  int32_t ex_p[kHuffThreads];       // exit position (segment-relative); then the block prefix
-  uint16_t ex_bk[kHuffThreads];     // exit (3b << 8) | k <= 27 * 256 + 63
+  int32_t ex_p[kHuffThreads];  // exit position (segment-relative)
+  int32_t en_p[kHuffThreads];  // entry of the slot's current trajectory
+  int32_t cp_p0[kHuffThreads], cp_p1[kHuffThreads]; // checkpoint positions
+  uint16_t ex_bk[kHuffThreads], en_bk[kHuffThreads]; // (3b << 8) | k
+  uint16_t cp_bk0[kHuffThreads], cp_bk1[kHuffThreads];
+  uint16_t cp_a0[kHuffThreads], cp_a1[kHuffThreads]; // blocks counted up to the checkpoints
+  uint16_t nblk[kHuffThreads]; // blocks started in the range (S <= kMaxParS bounds it)
+  uint16_t work[kHuffThreads]; // this round's slots to re-decode
+  uint8_t cp_n[kHuffThreads];
   int32_t seg_first[kMaxParSegs + 1]; // sub_first of the image's segments; [nseg] = slots
+  int32_t seg_pb[kMaxParSegs];        // segment start: bit position in the window
+  int32_t seg_nb[kMaxParSegs];        // segment length in bits
   int32_t scan[kHuffThreads / 64];
   int32_t any_changed;
   int32_t need_lanes, need_waves; // diagnostic counters (summed over rounds)
 };
-static_assert(sizeof(ImgLds) + 1024 <= kHuffStaticLds, "k_huff_image static LDS");
+static_assert(sizeof(ImgLds) + 512 <= kHuffStaticLds, "k_huff_image static LDS");
 
 // Exclusive prefix of v over the 1024-lane workgroup; contains __syncthreads.
 __device__ __forceinline__ int block_excl_scan1024(int v, int32_t *scratch, int *total) {
@@ -646,6 +615,51 @@ __device__ __forceinline__ int block_excl_scan1024(int v, int32_t *scratch, int 
   return base + inc - v;
 }
 
+// Where slot q of the image lies: its segment, subsequence index, window bit
+// position of the segment start, segment length and the range [rstart, stop).
+struct SlotGeom {
+  int si, j;
+  int32_t pbias, seg_bits, rstart, stop;
+};
+__device__ __forceinline__ SlotGeom slot_geom(const ImgLds &sh, int nseg, int S, int q) {
+  int lo = 0, hi = nseg - 1; // last segment with seg_first <= q
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (sh.seg_first[mid] <= q) lo = mid;
+    else hi = mid - 1;
+  }
+  SlotGeom g;
+  g.si = lo;
+  g.j = q - sh.seg_first[lo];
+  g.pbias = sh.seg_pb[lo];
+  g.seg_bits = sh.seg_nb[lo];
+  g.rstart = g.pbias + g.j * S;
+  g.stop = g.pbias + min((g.j + 1) * S, g.seg_bits);
+  return g;
+}
+
+__device__ __forceinline__ void put_cp(ImgLds &sh, int q, const Cp &cp) {
+  sh.cp_p0[q] = cp.p0;
+  sh.cp_p1[q] = cp.p1;
+  sh.cp_bk0[q] = (uint16_t)cp.bk0;
+  sh.cp_bk1[q] = (uint16_t)cp.bk1;
+  sh.cp_a0[q] = (uint16_t)cp.a0;
+  sh.cp_a1[q] = (uint16_t)cp.a1;
+  sh.cp_n[q] = (uint8_t)cp.n;
+}
+
+__device__ __forceinline__ Cp get_cp(const ImgLds &sh, int q) {
+  Cp cp;
+  cp.p0 = sh.cp_p0[q];
+  cp.p1 = sh.cp_p1[q];
+  cp.bk0 = sh.cp_bk0[q];
+  cp.bk1 = sh.cp_bk1[q];
+  cp.a0 = sh.cp_a0[q];
+  cp.a1 = sh.cp_a1[q];
+  cp.n = sh.cp_n[q];
+  return cp;
+}
+
 template <class W>
 __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
                                              const Segment *__restrict__ segs, const Dec &dec,
@@ -656,93 +670,103 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
                                              int32_t *__restrict__ dbg) {
   const int tid = threadIdx.x;
   const int S = d.sub_bits;
-  const bool live = tid < sh.seg_first[d.nseg];
-  int si = 0; // the lane's segment: last s with seg_first[s] <= tid
-  if (live) {
-    int lo = 0, hi = d.nseg - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (sh.seg_first[mid] <= tid) lo = mid;
-      else hi = mid - 1;
-    }
-    si = lo;
-  }
-  const Segment &sg = segs[d.seg_base + si];
-  const int j = tid - sh.seg_first[si];
-  const int32_t pbias = (int32_t)(sg.byte_start - d.dst_off) * 8; // window word 0 = dst_off
-  const int32_t seg_bits = (int32_t)((sg.byte_end - sg.byte_start) * 8);
-  const int32_t rstart = pbias + j * S;
-  const int32_t stop = pbias + min((j + 1) * S, seg_bits);
+  const int nseg = d.nseg;
+  const bool live = tid < sh.seg_first[nseg];
+  const SlotGeom g = slot_geom(sh, nseg, S, live ? tid : 0);
 
-  // ---- phase 1: decode from a guess, optionally `warm` bits early ----
-  int nblk = 0;
-  Cp cp, none;
-  cp.n = 0;
-  none.n = 0;
-  St st = make_state(0);
-  Rd<W> R;
-  R.src = src;
-  int en_p = 0, en_bk = 0; // entry state (segment-relative position)
-  if (live) {
-    const int32_t w0 = max(rstart - warm, pbias);
-    R.seek(w0);
-    if (w0 < rstart) {
-      int skipped = 0;
-      count_until(R, rstart, st, dec, skipped);
+  // ---- phase 1: every lane decodes its own range from a guess ----
+  {
+    int nblk = 0;
+    Cp cp, none;
+    cp.n = 0;
+    none.n = 0;
+    St st = make_state(0);
+    Rd<W> R;
+    R.src = src;
+    if (live) {
+      const int32_t w0 = max(g.rstart - warm, g.pbias);
+      R.seek(w0);
+      if (w0 < g.rstart) {
+        int skipped = 0;
+        count_until(R, g.rstart, st, dec, skipped);
+      }
+      sh.en_p[tid] = R.p - g.pbias;
+      sh.en_bk[tid] = (uint16_t)st.bk();
+      count_run<false>(R, g.rstart, g.stop, S, st, dec, nblk, cp, none, 0);
+      sh.ex_p[tid] = R.p - g.pbias;
+      sh.ex_bk[tid] = (uint16_t)st.bk();
+    } else {
+      sh.en_p[tid] = sh.ex_p[tid] = 0;
+      sh.en_bk[tid] = sh.ex_bk[tid] = 0;
     }
-    en_p = R.p - pbias;
-    en_bk = st.bk();
-    count_run<false>(R, rstart, stop, S, st, dec, nblk, cp, none, 0);
-    sh.ex_p[tid] = R.p - pbias;
-    sh.ex_bk[tid] = (uint16_t)st.bk();
-  } else {
-    sh.ex_p[tid] = 0;
-    sh.ex_bk[tid] = 0;
+    sh.nblk[tid] = (uint16_t)nblk;
+    put_cp(sh, tid, cp);
   }
 
-  // ---- rounds: re-decode while the entry differs from the predecessor's exit ----
+  // ---- rounds: re-decode every slot whose entry differs from its
+  // predecessor's exit, packed into the first waves ----
   int rounds = 0;
   uint64_t t_ph1 = 0;
+  const int wave = tid >> 6, lane = tid & 63;
   for (int round = 0; round <= kHuffThreads; ++round) {
     ++rounds;
+    __syncthreads(); // states published
+    if (round == 0 && tid == 0) t_ph1 = wall_clock64();
+    const bool need = live && g.j > 0 &&
+                      (sh.ex_p[tid - 1] != sh.en_p[tid] || sh.ex_bk[tid - 1] != sh.en_bk[tid]);
+    const uint64_t bal = __ballot(need);
+    if (lane == 0) sh.scan[wave] = __popcll(bal);
     __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kHuffThreads / 64; ++w) {
+      const int c = sh.scan[w];
+      base += w < wave ? c : 0;
+      tot += c;
+    }
+    if (need) sh.work[base + __popcll(bal & ((1ull << lane) - 1))] = (uint16_t)tid;
     if (tid == 0) {
       sh.any_changed = 0;
-      if (round == 0) t_ph1 = wall_clock64();
-    }
-    bool changed = false;
-    int np = 0, nbk = 0;
-    const bool need = live && j > 0 &&
-                      (sh.ex_p[tid - 1] != en_p || sh.ex_bk[tid - 1] != en_bk);
-    {
-      const uint64_t bal = __ballot(need);
-      if ((tid & 63) == 0 && bal) {
-        atomicAdd(&sh.need_lanes, __popcll(bal));
-        atomicAdd(&sh.need_waves, 1);
-      }
-    }
-    if (need) {
-      en_p = sh.ex_p[tid - 1];
-      en_bk = sh.ex_bk[tid - 1];
-      st = make_state(en_bk);
-      const int prev_total = nblk;
-      const Cp prev = cp;
-      nblk = 0;
-      R.seek(pbias + en_p);
-      if (count_run<true>(R, rstart, stop, S, st, dec, nblk, cp, prev, prev_total)) {
-        np = sh.ex_p[tid];
-        nbk = sh.ex_bk[tid];
-      } else {
-        np = R.p - pbias;
-        nbk = st.bk();
-      }
-      changed = (np != sh.ex_p[tid]) || (nbk != sh.ex_bk[tid]);
+      sh.need_lanes += tot;
+      sh.need_waves += (tot + 63) >> 6;
     }
     __syncthreads();
-    if (changed) {
-      sh.ex_p[tid] = np;
-      sh.ex_bk[tid] = (uint16_t)nbk;
-      sh.any_changed = 1;
+    if (tot == 0) break;
+    int q = -1, np = 0, nbk = 0, nb = 0, ep = 0, ebk = 0;
+    bool changed = false;
+    Cp cp;
+    cp.n = 0;
+    if (tid < tot) {
+      q = sh.work[tid];
+      const SlotGeom h = slot_geom(sh, nseg, S, q);
+      ep = sh.ex_p[q - 1];
+      ebk = sh.ex_bk[q - 1];
+      const Cp prev = get_cp(sh, q);
+      const int prev_total = sh.nblk[q];
+      St st = make_state(ebk);
+      Rd<W> R;
+      R.src = src;
+      R.seek(h.pbias + ep);
+      if (count_run<true>(R, h.rstart, h.stop, S, st, dec, nb, cp, prev, prev_total)) {
+        np = sh.ex_p[q];
+        nbk = sh.ex_bk[q];
+      } else {
+        np = R.p - h.pbias;
+        nbk = st.bk();
+      }
+      changed = (np != sh.ex_p[q]) || (nbk != sh.ex_bk[q]);
+    }
+    __syncthreads(); // every read of this round's exits is done
+    if (q >= 0) {
+      sh.en_p[q] = ep;
+      sh.en_bk[q] = (uint16_t)ebk;
+      sh.nblk[q] = (uint16_t)nb;
+      put_cp(sh, q, cp);
+      if (changed) {
+        sh.ex_p[q] = np;
+        sh.ex_bk[q] = (uint16_t)nbk;
+        sh.any_changed = 1;
+      }
     }
     __syncthreads();
     if (!sh.any_changed) break;
@@ -756,28 +780,31 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
 
   // ---- prefix of the block counts; the true entry is the predecessor's exit ----
   int wp = 0, wbk = 0;
-  if (live && j > 0) {
+  if (live && g.j > 0) {
     wp = sh.ex_p[tid - 1];
     wbk = sh.ex_bk[tid - 1];
   }
+  const Segment &sg = segs[d.seg_base + g.si];
   // the write pass ends where the next range starts: this lane's exit (a
   // count step may run past the range end); a segment's last range at its end
-  const int32_t wstop = j == sg.sub_count - 1 ? stop : pbias + sh.ex_p[tid];
+  const int32_t wstop = g.j == sg.sub_count - 1 ? g.stop : g.pbias + sh.ex_p[tid];
   int tot;
-  const int pre = block_excl_scan1024(live ? nblk : 0, sh.scan, &tot);
+  const int pre = block_excl_scan1024(live ? (int)sh.nblk[tid] : 0, sh.scan, &tot);
   sh.ex_p[tid] = pre;
   __syncthreads();
   const uint64_t t_scan = wall_clock64();
 
   // ---- write pass from the true entry ----
   if (live) {
-    int cursor = pre - sh.ex_p[sh.seg_first[si]] - 1; // segment-relative block, -1 before the DC
+    int cursor = pre - sh.ex_p[sh.seg_first[g.si]] - 1; // segment-relative block, -1 before the DC
     const int total = sg.mcu_count * d.bpm;
     const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
-    st = make_state(wbk);
-    R.seek(pbias + wp);
+    St st = make_state(wbk);
+    Rd<W> R;
+    R.src = src;
+    R.seek(g.pbias + wp);
     write_run(R, st, dec, wstop, cursor, total, coef + blk0 * 64, dcv + blk0);
-    if (j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
+    if (g.j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
   }
   // diagnostic phase times (10 ns ticks summed over images; ldt_debug_counters)
   __syncthreads();
@@ -795,37 +822,38 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
 __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
-    const int32_t *__restrict__ par_img, int win_bytes, int max_tabs, int warm_pct,
-    int16_t *__restrict__ coef,
-    int16_t *__restrict__ dcv, int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
+    const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
+    int16_t *__restrict__ coef, int16_t *__restrict__ dcv, int32_t *__restrict__ status,
+    int32_t *__restrict__ dbg) {
   __shared__ ImgLds sh;
   const int img = par_img[blockIdx.x];
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
   const uint64_t t_start = wall_clock64();
-  // dynamic LDS: [window win_bytes][count tables][kTabU16 tables]
-  LDS_AS uint32_t *cnt = (LDS_AS uint32_t *)(dyn_lds + win_bytes / 4);
-  Dec dec = load_dec(d, htabs, (lds_u16)(cnt + (max_tabs << kLookBits)), tid, kHuffThreads);
-  dec.cnt = cnt;
-  for (int s = tid; s < d.nseg; s += kHuffThreads) sh.seg_first[s] = segs[d.seg_base + s].sub_first;
+  // dynamic LDS: [window win_bytes][tables]
+  const Dec dec = load_dec(d, htabs, (lds_u16)(dyn_lds + win_bytes / 4), tid, kHuffThreads);
+  for (int s = tid; s < d.nseg; s += kHuffThreads) {
+    const Segment &sg = segs[d.seg_base + s];
+    sh.seg_first[s] = sg.sub_first;
+    sh.seg_pb[s] = (int32_t)(sg.byte_start - d.dst_off) * 8; // window word 0 = dst_off
+    sh.seg_nb[s] = (int32_t)((sg.byte_end - sg.byte_start) * 8);
+  }
   if (tid == 0) {
     const Segment &l = segs[d.seg_base + d.nseg - 1];
     sh.seg_first[d.nseg] = l.sub_first + l.sub_count;
     sh.need_lanes = 0;
     sh.need_waves = 0;
   }
-  __syncthreads(); // kTabU16 tables in LDS
-  build_count_tables(dec, cnt, tid, kHuffThreads);
   const int64_t need = destuff_region_bytes(d.src_len, d.nseg) + 16;
   const bool in_lds = need <= win_bytes;
   const uint8_t *base = dstuf + d.dst_off; // 16-aligned
   if (in_lds) {
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u *g = reinterpret_cast<const v4u *>(base);
+    const v4u *gsrc = reinterpret_cast<const v4u *>(base);
     LDS_AS v4u *wl = (LDS_AS v4u *)dyn_lds;
     for (int i = tid; i < (int)(need / 16); i += kHuffThreads) {
-      const v4u v = g[i];
+      const v4u v = gsrc[i];
       v4u o;
       o.x = __builtin_bswap32(v.x);
       o.y = __builtin_bswap32(v.y);
@@ -851,14 +879,10 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
   static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_huff_image),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kHuffLdsMax - kHuffStaticLds);
-  if (getenv("LDT_DEBUG_LAUNCH"))
-    fprintf(stderr, "k_huff_image attr=%d n_par=%d win=%d tabs=%d static=%zu\n", (int)attr, p.n_par,
-            p.win_bytes, huff_tab_lds(p.max_tabs) + huff_cnt_lds(p.max_tabs), sizeof(ImgLds));
   if (attr != hipSuccess) return attr;
-  const int tabs = p.max_tabs < 1 ? 1 : p.max_tabs;
-  const size_t lds = (size_t)p.win_bytes + huff_tab_lds(tabs) + huff_cnt_lds(tabs);
+  const size_t lds = (size_t)p.win_bytes + huff_tab_lds(p.max_tabs);
   hipLaunchKernelGGL(k_huff_image, dim3(p.n_par), dim3(kHuffThreads), lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.par_img, p.win_bytes, tabs, p.warm_pct, w.coef, w.dcv,
+                     p.htabs, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.dcv,
                      w.status, p.redo);
   return hipGetLastError();
 }

@@ -179,13 +179,14 @@ bool build_huff(const RawHuff &r, bool is_dc, HuffTab &t) {
   }
   // level 1 (unused codes: the invalid entry)
   const uint16_t invalid = huff_entry(16, 0, is_dc);
-  for (int q = 0; q < (1 << kLookBits); ++q) t.l1[q] = invalid;
+  static thread_local uint16_t l1[1 << kLookBits];
+  for (int q = 0; q < (1 << kLookBits); ++q) l1[q] = invalid;
   for (int q = 0; q < (kL2Chunks << kL2Bits); ++q) t.l2[q] = invalid;
   for (int j = 0; j < r.nsym; ++j) {
     if (lens[j] <= kLookBits) {
       const int shift = kLookBits - lens[j];
       const int base = codes[j] << shift;
-      for (int q = 0; q < (1 << shift); ++q) t.l1[base + q] = huff_entry(lens[j], r.syms[j], is_dc);
+      for (int q = 0; q < (1 << shift); ++q) l1[base + q] = huff_entry(lens[j], r.syms[j], is_dc);
     }
   }
   // level 2: one chunk per distinct kLookBits-bit prefix of a longer code
@@ -210,10 +211,31 @@ bool build_huff(const RawHuff &r, bool is_dc, HuffTab &t) {
       t.l2[(prefix_chunk[pre] << kL2Bits) + sub + q] = huff_entry(lens[j], r.syms[j], is_dc);
   }
   for (int q = 0; q < (1 << kLookBits); ++q)
-    if (prefix_chunk[q] >= 0) t.l1[q] = overflow ? (uint16_t)kHuffCanon : (uint16_t)(prefix_chunk[q] << 5);
+    if (prefix_chunk[q] >= 0) l1[q] = overflow ? (uint16_t)kHuffCanon : (uint16_t)(prefix_chunk[q] << 5);
   if (overflow) // every long-code prefix takes the canonical search
     for (int j = 0; j < r.nsym; ++j)
-      if (lens[j] > kLookBits) t.l1[codes[j] >> (lens[j] - kLookBits)] = (uint16_t)kHuffCanon;
+      if (lens[j] > kLookBits) l1[codes[j] >> (lens[j] - kLookBits)] = (uint16_t)kHuffCanon;
+  // count-mode entries (ldt_types.hpp HuffTab): runs of AC symbols whose
+  // codes all lie in the kLookBits peeked bits
+  const uint32_t mask = (1u << kLookBits) - 1;
+  for (uint32_t x = 0; x <= mask; ++x) {
+    const uint32_t e = l1[x];
+    uint32_t T = e & 31;
+    if (T == 0) {
+      t.lc[x] = e | (e << 16); // long code: the count entry is l1's indirect entry
+      continue;
+    }
+    uint32_t adv = e >> 9, pre = 0;
+    while (!is_dc && adv < 64 && adv <= 15 && T < (uint32_t)kLookBits) {
+      const uint32_t e2 = l1[(x << T) & mask];
+      const uint32_t t2 = e2 & 31;
+      if (t2 == 0 || T + (t2 - ((e2 >> 5) & 15)) > (uint32_t)kLookBits) break; // code past the peek
+      pre = adv;
+      adv += e2 >> 9;
+      T += t2;
+    }
+    t.lc[x] = e | ((T | (adv << 5) | (pre << 12)) << 16);
+  }
   return true;
 }
 

@@ -71,9 +71,10 @@ struct Segment {
 // lanes per image, one subsequence slot per lane. Images with more restart
 // segments than kMaxParSegs take the serial decoder (one lane per segment).
 constexpr int kHuffThreads = 1024;
-constexpr int kMaxParSegs = 512;
+constexpr int kMaxParSegs = 256;
+constexpr int kMaxParS = 32768;           // larger S (huge images): serial decoder
 constexpr int kHuffLdsMax = 160 * 1024;   // LDS per CU (gfx950)
-constexpr int kHuffStaticLds = 10 * 1024; // k_huff_image's static LDS (ImgLds) + margin
+constexpr int kHuffStaticLds = 38 * 1024; // k_huff_image's static LDS (ImgLds) + margin
 // Zero bytes after every destuffed segment (restart interval): a bit reader
 // may look up to 8 bytes past a segment without a bounds check and reads the
 // zeros libjpeg inserts at a marker (jdhuff.c jpeg_fill_bit_buffer).
@@ -99,15 +100,14 @@ constexpr int kDsChunkBytes = 4096;
 // entry (libjpeg: warning, 16 bits skipped, symbol 0).
 constexpr int kL2Chunks = 8;
 constexpr int kL2Bits = 16 - kLookBits;
-constexpr int kTabU16 = (1 << kLookBits) + (kL2Chunks << kL2Bits); // uint16 entries per table
 constexpr uint32_t kHuffCanon = 15u << 5;
+// A table in the decoders' LDS: lc (uint32 per kLookBits-bit peek: l1 entry in
+// the low half, count-mode entry in the high half), then l2 (uint16).
+constexpr int kL2Off = 2 << kLookBits;                      // l2 offset in uint16
+constexpr int kTabStride = kL2Off + (kL2Chunks << kL2Bits); // uint16 per table
 // LDS bytes of an image's distinct Huffman tables in the decoders
 __host__ __device__ inline int huff_tab_lds(int max_tabs) {
-  return (max_tabs < 1 ? 1 : max_tabs) * kTabU16 * 2;
-}
-// ... and of the parallel decoder's count-mode tables (uint32, 2^kLookBits each)
-__host__ __device__ inline int huff_cnt_lds(int max_tabs) {
-  return (max_tabs < 1 ? 1 : max_tabs) * (4 << kLookBits);
+  return (max_tabs < 1 ? 1 : max_tabs) * kTabStride * 2;
 }
 __host__ __device__ inline uint16_t huff_entry(int len, int sym, bool dc) {
   int s, adv;
@@ -121,8 +121,18 @@ __host__ __device__ inline uint16_t huff_entry(int len, int sym, bool dc) {
   }
   return (uint16_t)((len + s) | (s << 5) | (adv << 9));
 }
+// Count-mode entries (the parallel decoder's sync passes only count blocks,
+// so one lookup may consume several symbols), per kLookBits-bit peek:
+//   T (bits 0-4)    bits of the longest run of AC symbols of one block whose
+//                   codes all lie in the peeked bits (the last symbol's
+//                   magnitude may extend past them); DC tables: one symbol
+//   ADV (5-11)      coefficient advance of the run (an EOB, 64, ends it)
+//   PRE (12-15)     advance before the run's last symbol (<= 15): the run is
+//                   valid only if k + PRE < 64 (no block ends inside it);
+//                   otherwise the l1 entry (first symbol alone) applies
+// T == 0: a long code; the entry equals l1's indirect entry.
 struct HuffTab {
-  uint16_t l1[1 << kLookBits];
+  uint32_t lc[1 << kLookBits]; // l1 | cnt << 16
   uint16_t l2[kL2Chunks << kL2Bits];
   int32_t maxcode[18]; // [l] largest code of length l (-1 none), [17] sentinel
   int32_t valoff[18];

@@ -300,7 +300,7 @@ def test_huffman_decoder_modes(mode, bits, manifest):
 
 
 def test_many_restart_segments_take_serial_decoder():
-    """An image with more than 512 restart segments (a marker every MCU) goes
+    """An image with more than 256 restart segments (a marker every MCU) goes
     to the serial decoder while its batch-mates use the per-image parallel
     decoder; both bit-exact vs the oracle in one batch."""
     import ldt_amd
