@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <memory>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -157,9 +158,37 @@ struct ldt_ctx {
   int64_t stage_cnt[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
   EvSet *cur_ev = nullptr;
   int64_t last_off_redo = -1; // debug counters of the last batch (plan blob offset)
+  double host_us[4] = {0, 0, 0, 0}; // LDT_HOST_TIMING accumulators
+  int64_t host_calls = 0;
 };
 
 namespace {
+
+// Host-side phase times of decode_core (LDT_HOST_TIMING=1: averages printed
+// to stderr every 200 calls). Diagnostic only.
+struct HostTimer {
+  ldt_ctx *c;
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  explicit HostTimer(ldt_ctx *cc) : c(cc), on(host_timing_enabled()) {
+    if (on) t = std::chrono::steady_clock::now();
+  }
+  static bool host_timing_enabled() {
+    static const bool e = getenv("LDT_HOST_TIMING") != nullptr;
+    return e;
+  }
+  void mark(int k) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    c->host_us[k] += std::chrono::duration<double, std::micro>(n - t).count();
+    t = n;
+    if (k == 3 && ++c->host_calls % 30 == 0) {
+      fprintf(stderr, "ldt host us/call: parse %.1f plan %.1f copies %.1f launches %.1f\n",
+              c->host_us[0] / 30, c->host_us[1] / 30, c->host_us[2] / 30, c->host_us[3] / 30);
+      for (double &x : c->host_us) x = 0;
+    }
+  }
+};
 
 struct DeviceGuard {
   int prev = -1;
@@ -317,6 +346,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if ((rc = order_streams(c, s))) return rc;
 
   // ---- parse headers ----
+  HostTimer ht(c);
   const int64_t base = (int64_t)offsets[arr_offset];
   const int64_t total_bytes = (int64_t)offsets[arr_offset + n] - base;
   if (total_bytes < 0) return set_err(c, LDT_ERR_ARG, "offsets not monotonic");
@@ -607,6 +637,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     if (kv > max_ks_v) max_ks_v = kv;
   }
 
+  ht.mark(0); // headers parsed, per-image plans built
   // ---- plan blob layout ----
   PlanHdr ph;
   memset(&ph, 0, sizeof(ph));
@@ -680,6 +711,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if ((rc = ensure_dev(c, c->d_dcv, (size_t)coef_blocks * 2 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dscnt, 16 * (size_t)(n_chunks + 1), s))) return rc;
+  ht.mark(1); // plan blob written, buffers sized
   prof_begin(c, LDT_STAGE_H2D, s);
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
@@ -739,16 +771,18 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
   w.ds_cnt = static_cast<int4 *>(c->d_dscnt.p);
 
+  ht.mark(2); // copies enqueued
   HIPCHK(c, launch_destuff(p, w, s));
   prof_mark(c, LDT_STAGE_DESTUFF, s);
   HIPCHK(c, launch_huff_parallel(p, w, s));
   HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_prog(p, w, s));
-  HIPCHK(c, launch_dc_scan(p, w, s));
+  static const int exp_skip = getenv("LDT_EXP_SKIP") ? atoi(getenv("LDT_EXP_SKIP")) : 0; // EXPERIMENT
+  if (!(exp_skip & 1)) HIPCHK(c, launch_dc_scan(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
-  HIPCHK(c, launch_idct(p, w, s));
+  if (!(exp_skip & 2)) HIPCHK(c, launch_idct(p, w, s));
   prof_mark(c, LDT_STAGE_IDCT, s);
-  {
+  if (!(exp_skip & 4)) {
     hipError_t rerr = hipSuccess;
     if (!(c->resize_impl != 2 &&
           launch_resize4_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr)))
@@ -759,6 +793,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   prof_mark(c, LDT_STAGE_RESIZE, s);
   c->cur_ev = nullptr;
 
+  ht.mark(3); // kernels launched
   // ---- per-image status back to the host ----
   if ((size_t)n > c->h_status_cap) {
     if (c->h_status) HIPCHK(c, hipHostFree(c->h_status));

@@ -580,8 +580,10 @@ __device__ __forceinline__ bool count_run(Rd<W> &R, int32_t range_start, int32_t
 // the first waves of the workgroup (any lane may work on any slot).
 struct ImgLds {
   int32_t ex_p[kHuffThreads];  // exit position (segment-relative)
-  int32_t en_p[kHuffThreads];  // entry of the slot's current trajectory
-  int32_t cp_p0[kHuffThreads], cp_p1[kHuffThreads]; // checkpoint positions
+  // entry of the slot's current trajectory and its checkpoint positions,
+  // relative to the range start j*S (< S + 32 <= kMaxParS + 32)
+  uint16_t en_p[kHuffThreads];
+  uint16_t cp_p0[kHuffThreads], cp_p1[kHuffThreads];
   uint16_t ex_bk[kHuffThreads], en_bk[kHuffThreads]; // (3b << 8) | k
   uint16_t cp_bk0[kHuffThreads], cp_bk1[kHuffThreads];
   uint16_t cp_a0[kHuffThreads], cp_a1[kHuffThreads]; // blocks counted up to the checkpoints
@@ -638,9 +640,10 @@ __device__ __forceinline__ SlotGeom slot_geom(const ImgLds &sh, int nseg, int S,
   return g;
 }
 
-__device__ __forceinline__ void put_cp(ImgLds &sh, int q, const Cp &cp) {
-  sh.cp_p0[q] = cp.p0;
-  sh.cp_p1[q] = cp.p1;
+// checkpoint positions are reader positions; stored relative to the range start
+__device__ __forceinline__ void put_cp(ImgLds &sh, int q, const Cp &cp, int32_t rstart) {
+  sh.cp_p0[q] = (uint16_t)(cp.p0 - rstart);
+  sh.cp_p1[q] = (uint16_t)(cp.p1 - rstart);
   sh.cp_bk0[q] = (uint16_t)cp.bk0;
   sh.cp_bk1[q] = (uint16_t)cp.bk1;
   sh.cp_a0[q] = (uint16_t)cp.a0;
@@ -648,10 +651,10 @@ __device__ __forceinline__ void put_cp(ImgLds &sh, int q, const Cp &cp) {
   sh.cp_n[q] = (uint8_t)cp.n;
 }
 
-__device__ __forceinline__ Cp get_cp(const ImgLds &sh, int q) {
+__device__ __forceinline__ Cp get_cp(const ImgLds &sh, int q, int32_t rstart) {
   Cp cp;
-  cp.p0 = sh.cp_p0[q];
-  cp.p1 = sh.cp_p1[q];
+  cp.p0 = rstart + sh.cp_p0[q];
+  cp.p1 = rstart + sh.cp_p1[q];
   cp.bk0 = sh.cp_bk0[q];
   cp.bk1 = sh.cp_bk1[q];
   cp.a0 = sh.cp_a0[q];
@@ -690,17 +693,18 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
         int skipped = 0;
         count_until(R, g.rstart, st, dec, skipped);
       }
-      sh.en_p[tid] = R.p - g.pbias;
+      sh.en_p[tid] = (uint16_t)(R.p - g.rstart);
       sh.en_bk[tid] = (uint16_t)st.bk();
       count_run<false>(R, g.rstart, g.stop, S, st, dec, nblk, cp, none, 0);
       sh.ex_p[tid] = R.p - g.pbias;
       sh.ex_bk[tid] = (uint16_t)st.bk();
     } else {
-      sh.en_p[tid] = sh.ex_p[tid] = 0;
+      sh.en_p[tid] = 0;
+      sh.ex_p[tid] = 0;
       sh.en_bk[tid] = sh.ex_bk[tid] = 0;
     }
     sh.nblk[tid] = (uint16_t)nblk;
-    put_cp(sh, tid, cp);
+    put_cp(sh, tid, cp, g.rstart);
   }
 
   // ---- rounds: re-decode every slot whose entry differs from its
@@ -713,7 +717,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     __syncthreads(); // states published
     if (round == 0 && tid == 0) t_ph1 = wall_clock64();
     const bool need = live && g.j > 0 &&
-                      (sh.ex_p[tid - 1] != sh.en_p[tid] || sh.ex_bk[tid - 1] != sh.en_bk[tid]);
+                      (sh.ex_p[tid - 1] != (int)sh.en_p[tid] + g.j * S || sh.ex_bk[tid - 1] != sh.en_bk[tid]);
     const uint64_t bal = __ballot(need);
     if (lane == 0) sh.scan[wave] = __popcll(bal);
     __syncthreads();
@@ -733,15 +737,18 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     __syncthreads();
     if (tot == 0) break;
     int q = -1, np = 0, nbk = 0, nb = 0, ep = 0, ebk = 0;
+    int32_t qstart = 0, qj = 0; // the slot's range start: reader position, segment-relative
     bool changed = false;
     Cp cp;
     cp.n = 0;
     if (tid < tot) {
       q = sh.work[tid];
       const SlotGeom h = slot_geom(sh, nseg, S, q);
+      qstart = h.rstart;
+      qj = h.j * S;
       ep = sh.ex_p[q - 1];
       ebk = sh.ex_bk[q - 1];
-      const Cp prev = get_cp(sh, q);
+      const Cp prev = get_cp(sh, q, h.rstart);
       const int prev_total = sh.nblk[q];
       St st = make_state(ebk);
       Rd<W> R;
@@ -758,10 +765,10 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     }
     __syncthreads(); // every read of this round's exits is done
     if (q >= 0) {
-      sh.en_p[q] = ep;
+      sh.en_p[q] = (uint16_t)(ep - qj);
       sh.en_bk[q] = (uint16_t)ebk;
       sh.nblk[q] = (uint16_t)nb;
-      put_cp(sh, q, cp);
+      put_cp(sh, q, cp, qstart);
       if (changed) {
         sh.ex_p[q] = np;
         sh.ex_bk[q] = (uint16_t)nbk;

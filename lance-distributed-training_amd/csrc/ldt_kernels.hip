@@ -426,7 +426,7 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
 // The Huffman pass writes only nonzero AC coefficients; this kernel clears
 // every block it reads (also for images whose decode failed), so the buffer
 // needs no memset per batch (it is cleared once when allocated).
-constexpr int kIdctBlocksPerWg = 256;
+constexpr int kIdctBlocksPerWg = 128; // = threads; an 18 KB tile fits beside k_huff_image
 // jpeg_natural_order: zigzag position -> natural (row-major) index
 constexpr int kZigzagNat[64] = {
     0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
@@ -434,7 +434,7 @@ constexpr int kZigzagNat[64] = {
     30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 constexpr int kIdctTileStride = 36; // dwords per block in the LDS tile
 
-__global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
+__global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__restrict__ descs,
                                               const uint16_t *__restrict__ qtabs,
                                               int16_t *__restrict__ coef,
                                               const int16_t *__restrict__ dcv,
@@ -454,7 +454,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
   // coalesced: unit u = 16 bytes = row (u & 7) of block (u >> 3)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int u = i * 256 + tid;
+    const int u = i * kIdctBlocksPerWg + tid;
     if ((u >> 3) < nb) {
       if (ok) {
         const int4 v = gsrc[u];
@@ -465,7 +465,8 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc *__restrict__ descs,
   }
   if (!ok) return; // failed image: only restore the all-zero invariant
   // quant tables in zigzag order, like the coefficients
-  if (tid < 64 * d.ncomp) s_q[tid >> 6][tid & 63] = qtabs[d.qt[tid >> 6] * 64 + kZigzagNat[tid & 63]];
+  for (int i = tid; i < 64 * d.ncomp; i += kIdctBlocksPerWg)
+    s_q[i >> 6][i & 63] = qtabs[d.qt[i >> 6] * 64 + kZigzagNat[i & 63]];
   __syncthreads();
   if (tid >= nb) return;
   const int64_t blk = b0 + tid;
@@ -847,7 +848,7 @@ hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n == 0 || p.max_blocks == 0) return hipSuccess;
   dim3 grid((unsigned)((p.max_blocks + kIdctBlocksPerWg - 1) / kIdctBlocksPerWg), (unsigned)p.n);
-  hipLaunchKernelGGL(k_idct, grid, dim3(256), 0, s, p.descs, p.qtabs, w.coef, w.dcv, w.planes,
+  hipLaunchKernelGGL(k_idct, grid, dim3(kIdctBlocksPerWg), 0, s, p.descs, p.qtabs, w.coef, w.dcv, w.planes,
                      w.status);
   return hipGetLastError();
 }

@@ -151,6 +151,10 @@ struct Geom4 {
 };
 
 constexpr int kKvRows = 16; // vertical coefficient rows cached per wave
+// Waves (tasks) per workgroup: two keep a workgroup's LDS (3 KB LUT + two
+// wave areas, ~24 KB at 512 px) small enough to share a CU with the Huffman
+// decoder of another batch in flight.
+constexpr int kResizeWaves = 2;
 
 // SRC: 0 JPEG planes, 4:2:0 fast staging (resize_fast420 images only);
 // 2 JPEG planes, generic staging (the other images); 1 raw HWC rows, 16-byte
@@ -174,10 +178,10 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   constexpr bool kSkew = !kJpeg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
-  for (int i = tid; i < 768; i += 256) s_lut[i] = lut[i];
+  for (int i = tid; i < 768; i += (int)blockDim.x) s_lut[i] = lut[i];
   __syncthreads(); // the only workgroup barrier
   // wave-uniform task: descriptor loads become scalar loads into SGPRs
-  const int task = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wave);
+  const int task = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kResizeWaves + wave);
   if (task >= g.ntask) return;
   const int img = task / g.nbands, band = task - img * g.nbands;
   if (kJpeg && (status[img] != 0 || resize_fast420(descs[img]) != (SRC == 0))) return;
@@ -519,7 +523,7 @@ static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, 
   g.bh = (kOut + nb - 1) / nb;
   g.nbands = (kOut + g.bh - 1) / g.bh;
   g.ntask = n * g.nbands;
-  return 3072 + 4 * (size_t)g.wave_bytes <= 160 * 1024;
+  return 3072 + kResizeWaves * (size_t)g.wave_bytes <= 160 * 1024;
 }
 
 template <int SRC, int KS>
@@ -529,8 +533,9 @@ static hipError_t launch4(const ImgDesc *descs, const uint8_t *planes, RawSrc ra
   static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resize4<SRC, KS>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  const int groups = (g.ntask + 3) / 4;
-  hipLaunchKernelGGL((k_resize4<SRC, KS>), dim3(groups), dim3(256), 3072 + 4 * g.wave_bytes, s, descs,
+  const int groups = (g.ntask + kResizeWaves - 1) / kResizeWaves;
+  hipLaunchKernelGGL((k_resize4<SRC, KS>), dim3(groups), dim3(64 * kResizeWaves),
+                     3072 + kResizeWaves * g.wave_bytes, s, descs,
                      planes, raw, lut, labels, out, out_labels, status, g);
   return hipGetLastError();
 }
@@ -559,10 +564,10 @@ static int waves_target4(const Geom4 &g) {
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) cus = 256;
     else cus = prop.multiProcessorCount;
   }
-  int wg = (160 * 1024) / (3072 + 4 * g.wave_bytes);
-  if (wg > 3) wg = 3;
+  int wg = (160 * 1024) / (3072 + kResizeWaves * g.wave_bytes);
+  if (wg > 6) wg = 6;
   if (wg < 1) wg = 1;
-  return cus * 4 * wg;
+  return cus * kResizeWaves * wg;
 }
 
 bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,

@@ -11,17 +11,17 @@ from ldt_amd import _lib, synth  # noqa: E402
 
 ctx = _lib.get_context(0)
 names = ["redo", "wgs", "rounds_sum", "rounds_max", "walks", "walk_first", "walk_steps", "fallbacks",
-         "t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "need_lanes", "need_waves"]
+         "t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "need_lanes", "need_waves", "t_dc_idct"]
 for wl, fn, n in (("c2", synth.q90_512, 256), ("c1", synth.food101_like, 128), ("c4", synth.imagenet_like, 128)):
     cells, labels = fn(n, seed=1000)
     rb = ldt_amd.ResidentBatch(cells, labels)
     rb.decode()
     out = np.zeros(16, np.int32)
     ctx.check(ctx.lib.ldt_debug_counters(ctx.handle, out.ctypes.data, None), "dbg")
-    d = dict(zip(names, out[:15].tolist()))
+    d = dict(zip(names, out[:16].tolist()))
     w = max(d["wgs"], 1)
     d["rounds_avg"] = round(d["rounds_sum"] / w, 2)
-    for k in ("t_setup", "t_phase1", "t_rounds", "t_scan", "t_write"):
+    for k in ("t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "t_dc_idct"):
         d[k + "_us"] = round(d.pop(k) / w / 100.0, 2)  # 10 ns ticks per image
     d["need_lanes_per_round"] = round(d["need_lanes"] / max(d["rounds_sum"], 1), 1)
     d["need_waves_per_round"] = round(d["need_waves"] / max(d["rounds_sum"], 1), 2)
