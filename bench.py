@@ -67,7 +67,7 @@ def _rates(times, imgs):
     return {"best": round(r[-1], 1), "median": round(r[len(r) // 2], 1), "reps": [round(x, 1) for x in r]}
 
 
-def cpu_baseline(cells, labels, batch: int = 128, reps: int = 3):
+def cpu_baseline(cells, labels, batch: int = 128, reps: int = 5):
     """The reference's CPU path on this host, in this run.
 
     map-style legs: lance_map_style.py:54-69's harness, i.e. a stock torch
@@ -77,10 +77,9 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 3):
     pin_memory=True, persistent spawn workers; num_workers = 8 (the reference
     default, :137) and the box's CPU share. Each leg: one batch per worker
     (plus the prefetch queue) to warm up, then `reps` timed runs of
-    num_workers batches; best and median img/s.
+    2 x num_workers batches; best and median img/s.
     iterable leg: lance_iterable.py:38-50's decode_tensor_image on
     RecordBatches in the main process (num_workers=0, :75-77)."""
-    import importlib
     import shutil
     import tempfile
 
@@ -92,7 +91,8 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 3):
 
     from oracle import oracle
 
-    lds = importlib.import_module("ldt_amd.dataset")  # the package exports a dataset() function
+    import ldt_amd as lds
+
     tmp = tempfile.mkdtemp(prefix="ldt_cpu_")
     try:
         n = len(cells)
@@ -102,7 +102,7 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 3):
         host = len(os.sched_getaffinity(0))
         legs = []
         for w in sorted({8, min(host, CPU_SHARE)}):
-            need = batch * w * (2 + 2 + reps)  # warm-up + prefetch queue + timed
+            need = batch * w * (4 + 2 * reps)  # warm-up + timed
             order = [i % n for i in range(need)]
             loader = lds.get_safe_loader(ds, batch_size=batch, sampler=order, num_workers=w,
                                          collate_fn=oracle.pil_collate_fn, pin_memory=True,
@@ -113,13 +113,13 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 3):
             times = []
             for _ in range(reps):
                 t0 = time.perf_counter()
-                for _ in range(w):
+                for _ in range(2 * w):
                     out = next(it)
                 times.append(time.perf_counter() - t0)
             assert out["image"].shape == (batch, 3, 224, 224)
             del it, loader
             legs.append(dict(harness="map-style DataLoader(SafeLanceDataset, PIL collate_fn)",
-                             num_workers=w, batch=batch, **_rates(times, batch * w)))
+                             num_workers=w, batch=batch, **_rates(times, 2 * batch * w)))
         rb = pa.RecordBatch.from_arrays([pa.array(cells[:batch], pa.binary()),
                                          pa.array(np.asarray(labels[:batch], np.int64))],
                                         names=["image", "label"])
@@ -138,7 +138,7 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 3):
         "value": ref["median"], "unit": "img/s", "cores": ref["num_workers"], "kind": "reference",
         "sample": (f"the reference CPU path on this workload's cells: DataLoader(SafeLanceDataset shim, "
                    f"PIL collate_fn, batch {batch}, pin_memory, persistent spawn workers), "
-                   f"{reps} x num_workers timed batches per leg after warm-up; Pillow {pil_version} / "
+                   f"{reps} x 2*num_workers timed batches per leg after warm-up; Pillow {pil_version} / "
                    f"libjpeg-turbo {features.version_feature('libjpeg_turbo')}; host affinity {host} CPUs "
                    f"(a one-GPU run may use {CPU_SHARE}); value = median of the "
                    f"num_workers={ref['num_workers']} leg (lance_map_style.py:137 default)"),

@@ -74,6 +74,12 @@ def raw_hwc(n: int, h: int = 1024, w: int = 1024, seed: int = 0) -> np.ndarray:
     return np.random.RandomState(seed).randint(0, 256, size=(n, h, w, 3), dtype=np.uint8)
 
 
+def raw_hwc_one(h: int, w: int, seed: int) -> np.ndarray:
+    """One raw uint8 HWC cell (seeded uniform), for full-batch parity runs
+    that build a large batch image by image."""
+    return np.random.RandomState(seed).randint(0, 256, size=(h, w, 3), dtype=np.uint8)
+
+
 def arrow_batch(cells: Sequence[bytes], labels) -> "pa.RecordBatch":
     import pyarrow as pa
 

@@ -1,0 +1,53 @@
+"""Multi-rank sampler + decode path with the device kernels (VERDICT r1 item
+7): world size 2, gloo, both ranks on cuda:0, the reference's iterable setup
+(lance_iterable.py:61-69,80) over a FOOD101-shaped fragment list scaled down
+50x ([250] * 6 + [15] rows, batch 8): ShardedFragmentSampler(pad=True) plans
+on the device and agrees on the padded batch count with one all_reduce(MAX);
+decode_tensor_image decodes every batch. Scaling stays unmeasured here (one
+GPU); the 8-GPU runs are the driver's."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FRAGS = [250] * 6 + [15]
+B = 8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_fragment_sampler_pad_decode(tmp_path):
+    import pyarrow as pa
+    import torch.multiprocessing as mp
+
+    import ldt_amd
+    import _dist_gpu_worker
+    from ldt_amd import synth
+
+    n = sum(FRAGS)
+    cells = [synth.encode(synth.field(40 + (i % 5) * 8, 48 + (i % 3) * 8, 5000 + i, 6.0)) for i in range(n)]
+    uri = str(tmp_path / "food_small")
+    ldt_amd.write_dataset(
+        pa.table({"image": pa.array(cells, pa.binary()), "label": pa.array(np.arange(n, dtype=np.int64))}),
+        uri, max_rows_per_file=250)
+    assert [f.count_rows() for f in ldt_amd.dataset(uri).get_fragments()] == FRAGS
+    mp.start_processes(_dist_gpu_worker.run, args=(2, _free_port(), uri, str(tmp_path)), nprocs=2,
+                       join=True, start_method="spawn")
+    r = [json.load(open(tmp_path / f"gpu_rank{k}.json")) for k in range(2)]
+    # rank 0: fragments 0,2,4,6 -> 32*3 + 2 = 98 batches; rank 1: 1,3,5 -> 96,
+    # padded to 98 (this build's rule: a short rank re-yields its own batches)
+    assert r[0]["batches"] == r[1]["batches"] == 98
+    seen = [set(x for b in r[k]["labels"] for x in b) for k in range(2)]
+    assert not (seen[0] & seen[1]), "ranks share rows"
+    assert sorted(seen[0] | seen[1]) == list(range(n)), "rows missing"
+    assert r[0]["bad"] == [] and r[1]["bad"] == [], "decoded images differ from the oracle"

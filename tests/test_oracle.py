@@ -138,3 +138,21 @@ def test_randperm_restatement_vs_torch(n, seed):
     g = torch.Generator()
     g.manual_seed(seed)
     assert torch.randperm(n, generator=g).tolist() == oracle.randperm(n, seed % (1 << 64)).tolist()
+
+
+def test_fullbatch_fixture_matches_oracle():
+    """tests/golden/fullbatch.json (full-batch GPU parity) agrees with the
+    oracle on its first images of both configs."""
+    import hashlib
+    import json
+
+    from ldt_amd import synth
+
+    g = json.load(open(os.path.join(GOLDEN, "fullbatch.json")))
+    cells, labels = synth.q90_512(3, seed=g["seed"])
+    for k, b in enumerate(cells):
+        assert hashlib.sha256(oracle.jpeg_to_tensor(b).tobytes()).hexdigest() == g["c2"]["sha256"][k]
+    for i in range(2):
+        raw = synth.raw_hwc_one(1024, 1024, g["seed"] * 100003 + i)
+        assert hashlib.sha256(oracle.raw_to_tensor(raw, normalize=True).tobytes()).hexdigest() == \
+            g["c5"]["sha256"][i]
