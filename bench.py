@@ -371,7 +371,7 @@ def main():
         dist.destroy_process_group()
 
 
-PROFILE_ROUND = "r1"
+PROFILE_ROUND = "r2"
 
 
 def load_profile(name: str):

@@ -777,12 +777,11 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   HIPCHK(c, launch_huff_parallel(p, w, s));
   HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_prog(p, w, s));
-  static const int exp_skip = getenv("LDT_EXP_SKIP") ? atoi(getenv("LDT_EXP_SKIP")) : 0; // EXPERIMENT
-  if (!(exp_skip & 1)) HIPCHK(c, launch_dc_scan(p, w, s));
+  HIPCHK(c, launch_dc_scan(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
-  if (!(exp_skip & 2)) HIPCHK(c, launch_idct(p, w, s));
+  HIPCHK(c, launch_idct(p, w, s));
   prof_mark(c, LDT_STAGE_IDCT, s);
-  if (!(exp_skip & 4)) {
+  {
     hipError_t rerr = hipSuccess;
     if (!(c->resize_impl != 2 &&
           launch_resize4_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr)))

@@ -422,9 +422,10 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
 // stride 144 B: conflict-free ds_read_b128 per lane), and zeros are written
 // back with the same coalesced stores.
 //
-// Coefficient buffer contract (with k_huff_write): all zero between batches.
-// The Huffman pass writes only nonzero AC coefficients; this kernel clears
-// every block it reads (also for images whose decode failed), so the buffer
+// Coefficient buffer contract (with the Huffman decoders and k_prog): all
+// zero between batches. The Huffman pass writes only nonzero AC coefficient
+// groups; this kernel reads every block (also of images whose decode failed)
+// and writes zeros back over the groups that are not zero, so the buffer
 // needs no memset per batch (it is cleared once when allocated).
 constexpr int kIdctBlocksPerWg = 128; // = threads; an 18 KB tile fits beside k_huff_image
 // jpeg_natural_order: zigzag position -> natural (row-major) index
@@ -456,11 +457,11 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
   for (int i = 0; i < 8; ++i) {
     const int u = i * kIdctBlocksPerWg + tid;
     if ((u >> 3) < nb) {
-      if (ok) {
-        const int4 v = gsrc[u];
-        *reinterpret_cast<int4 *>(&s_tile[(u >> 3) * kIdctTileStride + (u & 7) * 4]) = v;
-      }
-      gsrc[u] = make_int4(0, 0, 0, 0);
+      // restore the all-zero invariant: only groups that hold coefficients
+      // are written back (a failed image's blocks are read for that too)
+      const int4 v = gsrc[u];
+      if (ok) *reinterpret_cast<int4 *>(&s_tile[(u >> 3) * kIdctTileStride + (u & 7) * 4]) = v;
+      if ((v.x | v.y | v.z | v.w) != 0) gsrc[u] = make_int4(0, 0, 0, 0);
     }
   }
   if (!ok) return; // failed image: only restore the all-zero invariant
