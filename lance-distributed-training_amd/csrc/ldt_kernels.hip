@@ -417,23 +417,21 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
 
 // One lane per 8x8 block: the whole block stays in registers for both
 // passes (no transposes, no barriers between them). A workgroup covers
-// kIdctBlocksPerWg consecutive blocks of one image; their 32 KB of
-// coefficients are read with coalesced 16-byte loads into an LDS tile (block
-// stride 144 B: conflict-free ds_read_b128 per lane), and zeros are written
-// back with the same coalesced stores.
+// kIdctBlocksPerWg consecutive blocks of one image; each lane loads its
+// block's 128-B line straight into registers (no LDS tile: occupancy is set by
+// registers alone, so more blocks are in flight).
 //
 // Coefficient buffer contract (with the Huffman decoders and k_prog): all
 // zero between batches. The Huffman pass writes only nonzero AC coefficient
 // groups; this kernel reads every block (also of images whose decode failed)
 // and writes zeros back over the groups that are not zero, so the buffer
 // needs no memset per batch (it is cleared once when allocated).
-constexpr int kIdctBlocksPerWg = 128; // = threads; an 18 KB tile fits beside k_huff_image
+constexpr int kIdctBlocksPerWg = 256; // = threads
 // jpeg_natural_order: zigzag position -> natural (row-major) index
 constexpr int kZigzagNat[64] = {
     0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
     41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
     30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-constexpr int kIdctTileStride = 36; // dwords per block in the LDS tile
 
 __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__restrict__ descs,
                                               const uint16_t *__restrict__ qtabs,
@@ -441,7 +439,6 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
                                               const int16_t *__restrict__ dcv,
                                               uint8_t *__restrict__ planes,
                                               const int32_t *__restrict__ status) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_tile[kIdctBlocksPerWg * kIdctTileStride];
   __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
   const int img = blockIdx.y;
   const ImgDesc &d = descs[img];
@@ -451,26 +448,23 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
   const int tid = threadIdx.x;
   const bool ok = status[img] == 0;
   const int nb = (int)min((int64_t)kIdctBlocksPerWg, nblk - b0);
-  int4 *gsrc = reinterpret_cast<int4 *>(coef + (d.coef_off + b0) * 64);
-  // coalesced: unit u = 16 bytes = row (u & 7) of block (u >> 3)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int u = i * kIdctBlocksPerWg + tid;
-    if ((u >> 3) < nb) {
-      // restore the all-zero invariant: only groups that hold coefficients
-      // are written back (a failed image's blocks are read for that too)
-      const int4 v = gsrc[u];
-      if (ok) *reinterpret_cast<int4 *>(&s_tile[(u >> 3) * kIdctTileStride + (u & 7) * 4]) = v;
-      if ((v.x | v.y | v.z | v.w) != 0) gsrc[u] = make_int4(0, 0, 0, 0);
-    }
-  }
-  if (!ok) return; // failed image: only restore the all-zero invariant
   // quant tables in zigzag order, like the coefficients
   for (int i = tid; i < 64 * d.ncomp; i += kIdctBlocksPerWg)
     s_q[i >> 6][i & 63] = qtabs[d.qt[i >> 6] * 64 + kZigzagNat[i & 63]];
   __syncthreads();
   if (tid >= nb) return;
   const int64_t blk = b0 + tid;
+  // the lane's block straight into registers (one 128-B line per lane), and
+  // zeros back over the groups that held coefficients (the all-zero
+  // invariant; a failed image's blocks are cleared too)
+  uint4 *src = reinterpret_cast<uint4 *>(coef + (d.coef_off + blk) * 64);
+  uint4 raw[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) raw[r] = src[r];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+    if ((raw[r].x | raw[r].y | raw[r].z | raw[r].w) != 0) src[r] = make_uint4(0u, 0u, 0u, 0u);
+  if (!ok) return;
   const int64_t m = blk / d.bpm;
   const int b = (int)(blk - m * d.bpm);
   const int comp = d.bcomp[b];
@@ -478,12 +472,10 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
   // dequantised block, row-major (jidctint.c DEQUANTIZE); the stored slots
   // are in zigzag order (k_huff_write), placed at their natural index here
   int32_t ws[64];
-  const uint32_t *tl = &s_tile[tid * kIdctTileStride];
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    const uint4 raw = *reinterpret_cast<const uint4 *>(tl + 4 * r);
     const uint4 q4 = *reinterpret_cast<const uint4 *>(q + 8 * r);
-    const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+    const uint32_t rw[4] = {raw[r].x, raw[r].y, raw[r].z, raw[r].w};
     const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
