@@ -158,7 +158,7 @@ struct ldt_ctx {
   int64_t stage_cnt[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
   EvSet *cur_ev = nullptr;
   int64_t last_off_redo = -1; // debug counters of the last batch (plan blob offset)
-  double host_us[4] = {0, 0, 0, 0}; // LDT_HOST_TIMING accumulators
+  double host_us[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}; // LDT_HOST_TIMING accumulators
   int64_t host_calls = 0;
 };
 
@@ -182,9 +182,11 @@ struct HostTimer {
     const auto n = std::chrono::steady_clock::now();
     c->host_us[k] += std::chrono::duration<double, std::micro>(n - t).count();
     t = n;
-    if (k == 3 && ++c->host_calls % 30 == 0) {
-      fprintf(stderr, "ldt host us/call: parse %.1f plan %.1f copies %.1f launches %.1f\n",
-              c->host_us[0] / 30, c->host_us[1] / 30, c->host_us[2] / 30, c->host_us[3] / 30);
+    if (k == 5 && ++c->host_calls % 30 == 0) {
+      fprintf(stderr,
+              "ldt host us/call: parse %.1f slot-wait %.1f plan %.1f copies %.1f (cells %.1f memcpy+record %.1f prof_begin %.1f) launches %.1f status %.1f\n",
+              c->host_us[0] / 30, c->host_us[1] / 30, c->host_us[2] / 30, c->host_us[3] / 30,
+              c->host_us[6] / 30, c->host_us[7] / 30, c->host_us[8] / 30, c->host_us[4] / 30, c->host_us[5] / 30);
       for (double &x : c->host_us) x = 0;
     }
   }
@@ -681,6 +683,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   ph.total_blocks = coef_blocks;
 
   if ((rc = acquire_slot(c))) return rc;
+  ht.mark(1); // pinned slot free
   const int sl = c->slot;
   if ((rc = ensure_pin(c, c->h_plan[sl], (size_t)plan_bytes))) return rc;
   uint8_t *hp = static_cast<uint8_t *>(c->h_plan[sl].p);
@@ -711,8 +714,15 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if ((rc = ensure_dev(c, c->d_dcv, (size_t)coef_blocks * 2 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dscnt, 16 * (size_t)(n_chunks + 1), s))) return rc;
-  ht.mark(1); // plan blob written, buffers sized
+  ht.mark(2); // plan blob written, buffers sized
+  auto tick = [&](int k, std::chrono::steady_clock::time_point &t0) {
+    const auto t1 = std::chrono::steady_clock::now();
+    if (ht.on) c->host_us[k] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    t0 = t1;
+  };
+  auto t0 = std::chrono::steady_clock::now();
   prof_begin(c, LDT_STAGE_H2D, s);
+  tick(8, t0);
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
     if ((rc = ensure_pin(c, c->h_data[sl], (size_t)total_bytes + 16))) return rc;
@@ -722,10 +732,13 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
                              hipMemcpyHostToDevice, s));
     dev_cells = static_cast<const uint8_t *>(c->d_data.p);
   }
+  tick(6, t0);
   HIPCHK(c, hipMemcpyAsync(c->d_plan.p, hp, (size_t)plan_bytes, hipMemcpyHostToDevice, s));
+  tick(7, t0);
   HIPCHK(c, hipEventRecord(c->slot_ev[sl], s));
   c->slot_used[sl] = true;
   prof_mark(c, LDT_STAGE_H2D, s);
+  tick(7, t0);
 
   uint8_t *dp = static_cast<uint8_t *>(c->d_plan.p);
   DevPlan p;
@@ -771,7 +784,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
   w.ds_cnt = static_cast<int4 *>(c->d_dscnt.p);
 
-  ht.mark(2); // copies enqueued
+  ht.mark(3); // copies enqueued
   HIPCHK(c, launch_destuff(p, w, s));
   prof_mark(c, LDT_STAGE_DESTUFF, s);
   HIPCHK(c, launch_huff_parallel(p, w, s));
@@ -792,7 +805,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   prof_mark(c, LDT_STAGE_RESIZE, s);
   c->cur_ev = nullptr;
 
-  ht.mark(3); // kernels launched
+  ht.mark(4); // kernels launched
   // ---- per-image status back to the host ----
   if ((size_t)n > c->h_status_cap) {
     if (c->h_status) HIPCHK(c, hipHostFree(c->h_status));
@@ -804,6 +817,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   HIPCHK(c, hipMemcpyAsync(c->h_status, w.status, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
   c->last_n = n;
   if ((rc = finish_call(c, s))) return rc;
+  ht.mark(5); // status copy enqueued
   memcpy(status_out, st.data(), 4 * (size_t)n);
   if (c->sync_status) {
     HIPCHK(c, hipStreamSynchronize(s));

@@ -589,13 +589,17 @@ struct ImgLds {
   uint16_t cp_a0[kHuffThreads], cp_a1[kHuffThreads]; // blocks counted up to the checkpoints
   uint16_t nblk[kHuffThreads]; // blocks started in the range (S <= kMaxParS bounds it)
   uint16_t work[kHuffThreads]; // this round's slots to re-decode
+  // the slot's previous trajectory (memo): entry, exit (relative to the range
+  // start) and block count; m_en_bk = 0xFFFF: none
+  uint16_t m_en_p[kHuffThreads], m_en_bk[kHuffThreads];
+  uint16_t m_ex_p[kHuffThreads], m_ex_bk[kHuffThreads], m_nblk[kHuffThreads];
   uint8_t cp_n[kHuffThreads];
   int32_t seg_first[kMaxParSegs + 1]; // sub_first of the image's segments; [nseg] = slots
   int32_t seg_pb[kMaxParSegs];        // segment start: bit position in the window
   int32_t seg_nb[kMaxParSegs];        // segment length in bits
   int32_t scan[kHuffThreads / 64];
   int32_t any_changed;
-  int32_t need_lanes, need_waves; // diagnostic counters (summed over rounds)
+  int32_t need_lanes, need_waves, memo_hits; // diagnostic counters (summed over rounds)
 };
 static_assert(sizeof(ImgLds) + 512 <= kHuffStaticLds, "k_huff_image static LDS");
 
@@ -704,6 +708,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
       sh.en_bk[tid] = sh.ex_bk[tid] = 0;
     }
     sh.nblk[tid] = (uint16_t)nblk;
+    sh.m_en_bk[tid] = 0xFFFF;
     put_cp(sh, tid, cp, g.rstart);
   }
 
@@ -716,6 +721,37 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     ++rounds;
     __syncthreads(); // states published
     if (round == 0 && tid == 0) t_ph1 = wall_clock64();
+    // A slot whose predecessor's exit equals the entry of its previous
+    // trajectory adopts that trajectory again (exits flip between two values
+    // while an unsynchronised stretch converges); repeated until no slot
+    // changes, so a run of such slots resolves without decoding.
+    for (;;) {
+      bool hit = false;
+      if (live && g.j > 0) {
+        const int rel = sh.ex_p[tid - 1] - g.j * S;
+        const int pbk = sh.ex_bk[tid - 1];
+        hit = (rel != (int)sh.en_p[tid] || pbk != (int)sh.en_bk[tid]) && rel == (int)sh.m_en_p[tid] &&
+              pbk == (int)sh.m_en_bk[tid];
+      }
+      __syncthreads(); // every read of the exits is done
+      if (hit) {
+        const uint16_t ep = sh.en_p[tid], ebk = sh.en_bk[tid], nb = sh.nblk[tid], xbk = sh.ex_bk[tid];
+        const int xp = sh.ex_p[tid];
+        sh.en_p[tid] = sh.m_en_p[tid];
+        sh.en_bk[tid] = sh.m_en_bk[tid];
+        sh.ex_p[tid] = (int)sh.m_ex_p[tid] + g.j * S;
+        sh.ex_bk[tid] = sh.m_ex_bk[tid];
+        sh.nblk[tid] = sh.m_nblk[tid];
+        sh.m_en_p[tid] = ep;
+        sh.m_en_bk[tid] = ebk;
+        sh.m_ex_p[tid] = (uint16_t)(xp - g.j * S);
+        sh.m_ex_bk[tid] = xbk;
+        sh.m_nblk[tid] = nb;
+        sh.cp_n[tid] = 0; // the adopted trajectory's checkpoints are not kept
+        atomicAdd(&sh.memo_hits, 1);
+      }
+      if (!__syncthreads_or(hit)) break;
+    }
     const bool need = live && g.j > 0 &&
                       (sh.ex_p[tid - 1] != (int)sh.en_p[tid] + g.j * S || sh.ex_bk[tid - 1] != sh.en_bk[tid]);
     const uint64_t bal = __ballot(need);
@@ -765,6 +801,12 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     }
     __syncthreads(); // every read of this round's exits is done
     if (q >= 0) {
+      // the trajectory being replaced becomes the slot's memo
+      sh.m_en_p[q] = sh.en_p[q];
+      sh.m_en_bk[q] = sh.en_bk[q];
+      sh.m_ex_p[q] = (uint16_t)(sh.ex_p[q] - qj);
+      sh.m_ex_bk[q] = sh.ex_bk[q];
+      sh.m_nblk[q] = sh.nblk[q];
       sh.en_p[q] = (uint16_t)(ep - qj);
       sh.en_bk[q] = (uint16_t)ebk;
       sh.nblk[q] = (uint16_t)nb;
@@ -823,6 +865,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     atomicAdd(dbg + 12, (int)(t_end - t_scan));
     atomicAdd(dbg + 13, sh.need_lanes);
     atomicAdd(dbg + 14, sh.need_waves);
+    atomicAdd(dbg + 4, sh.memo_hits);
   }
 }
 
@@ -851,6 +894,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     sh.seg_first[d.nseg] = l.sub_first + l.sub_count;
     sh.need_lanes = 0;
     sh.need_waves = 0;
+    sh.memo_hits = 0;
   }
   const int64_t need = destuff_region_bytes(d.src_len, d.nseg) + 16;
   const bool in_lds = need <= win_bytes;

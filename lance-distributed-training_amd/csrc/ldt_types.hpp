@@ -74,7 +74,7 @@ constexpr int kHuffThreads = 1024;
 constexpr int kMaxParSegs = 256;
 constexpr int kMaxParS = 32768;           // larger S (huge images): serial decoder
 constexpr int kHuffLdsMax = 160 * 1024;   // LDS per CU (gfx950)
-constexpr int kHuffStaticLds = 32 * 1024; // k_huff_image's static LDS (ImgLds) + margin
+constexpr int kHuffStaticLds = 42 * 1024; // k_huff_image's static LDS (ImgLds) + margin
 // Zero bytes after every destuffed segment (restart interval): a bit reader
 // may look up to 8 bytes past a segment without a bounds check and reads the
 // zeros libjpeg inserts at a marker (jdhuff.c jpeg_fill_bit_buffer).

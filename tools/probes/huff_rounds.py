@@ -10,7 +10,7 @@ import ldt_amd  # noqa: E402
 from ldt_amd import _lib, synth  # noqa: E402
 
 ctx = _lib.get_context(0)
-names = ["redo", "wgs", "rounds_sum", "rounds_max", "walks", "walk_first", "walk_steps", "fallbacks",
+names = ["redo", "wgs", "rounds_sum", "rounds_max", "memo_hits", "walk_first", "walk_steps", "fallbacks",
          "t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "need_lanes", "need_waves", "t_dc_idct"]
 for wl, fn, n in (("c2", synth.q90_512, 256), ("c1", synth.food101_like, 128), ("c4", synth.imagenet_like, 128)):
     cells, labels = fn(n, seed=1000)
