@@ -97,11 +97,11 @@ struct Rd {
   }
   __device__ __forceinline__ void consume(int t) { // t <= 31
     p += t;
-    rs -= t;
-    const bool m = rs < 0;
+    const int32_t r2 = rs - t;
+    const bool m = r2 < 0;
     hi = m ? lo : hi;
     lo = m ? nxt : lo;
-    rs = m ? rs + 32 : rs;
+    rs = r2 & 31;
     wi += m ? 1 : 0;
     nxt = src(wi);
   }
@@ -112,7 +112,8 @@ struct Rd {
 // (b3, k): 3 * (block within the MCU) and the coefficient index (0: DC next).
 // ---------------------------------------------------------------------------
 struct Dec {
-  lds_cu16 tabs;     // the image's distinct tables, kTabStride uint16 per slot
+  lds_cu8 tabs;      // the image's distinct tables: lc of slot s at byte s << 13,
+                     // l2 of slot s at byte (ns << 13) + s * kL2Bytes
   uint32_t dcseq;    // LDS table slot of MCU block b's DC table at bits 3b
   uint32_t acseq;    // ... AC table
   int b3end;         // 3 * blocks per MCU
@@ -121,6 +122,10 @@ struct Dec {
   const HuffTab *g;  // plan tables (canonical fallback)
   const ImgDesc *d;
 };
+
+constexpr int kLcBytes = 4 << kLookBits;              // lc part of a table in LDS
+constexpr int kL2Bytes = 2 * (kL2Chunks << kL2Bits);  // l2 part
+static_assert(kLcBytes == 1 << 13, "lc slot stride is a shift by 13");
 
 struct St {
   int b3, k;
@@ -156,19 +161,23 @@ __device__ __forceinline__ int image_slots(const ImgDesc &d, uint32_t &slotmap, 
 }
 
 // Copy an image's distinct tables into LDS and return the decode constants.
+// lc parts at an 8 KB stride (the slot's offset is one shift), l2 parts after
+// them.
 __device__ __forceinline__ Dec load_dec(const ImgDesc &d, const HuffTab *__restrict__ htabs,
-                                        lds_u16 tabs, int tid, int nthreads) {
+                                        LDS_AS uint8_t *tabs, int tid, int nthreads) {
   int slot_tab[6];
   uint32_t slotmap;
   const int ns = image_slots(d, slotmap, slot_tab);
-  constexpr int kWords = kTabStride / 2;
+  constexpr int kWords = (kLcBytes + kL2Bytes) / 4; // HuffTab: lc then l2
   for (int i = tid; i < ns * kWords; i += nthreads) {
     const int q = i / kWords, o = i - q * kWords;
     int tix = slot_tab[0];
 #pragma unroll
     for (int x = 1; x < 6; ++x)
       if (q == x) tix = slot_tab[x];
-    ((LDS_AS uint32_t *)(tabs + q * kTabStride))[o] = reinterpret_cast<const uint32_t *>(htabs + tix)[o];
+    const uint32_t v = reinterpret_cast<const uint32_t *>(htabs + tix)[o];
+    const int dst = o < kLcBytes / 4 ? (q << 13) + 4 * o : (ns << 13) + q * kL2Bytes + 4 * o - kLcBytes;
+    *(LDS_AS uint32_t *)(tabs + dst) = v;
   }
   Dec dec;
   dec.tabs = tabs;
@@ -202,18 +211,21 @@ __device__ __attribute__((noinline)) uint32_t lookup_canon(const HuffTab *__rest
   return huff_entry(16, 0, !ac);
 }
 
+// Second level of a long code (l1 entry e1: total == 0).
+__device__ __forceinline__ uint32_t lookup_long(const Dec &dec, uint32_t slot, uint32_t e1, uint32_t pk,
+                                                int b3, bool ac) {
+  if (e1 == kHuffCanon) return lookup_canon(dec.g, dec.d, b3 / 3, ac, pk);
+  const lds_cu16 l2 = (lds_cu16)(dec.tabs + (dec.ns << 13) + slot * kL2Bytes);
+  return l2[((e1 >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
+}
+
 // Entry of the symbol whose code starts at the top bit of pk.
 __device__ __forceinline__ uint32_t lookup(const Dec &dec, const St &st, uint32_t pk) {
   const bool ac = st.k != 0;
   const uint32_t slot = __builtin_amdgcn_ubfe(ac ? dec.acseq : dec.dcseq, (uint32_t)st.b3, 3u);
-  const lds_cu16 t = dec.tabs + slot * kTabStride;
-  uint32_t e = ((const LDS_AS uint32_t *)t)[pk >> (32 - kLookBits)] & 0xFFFFu;
-  if (__builtin_expect((e & 31) == 0, 0)) {
-    if (e != kHuffCanon)
-      e = t[kL2Off + ((e >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
-    else
-      e = lookup_canon(dec.g, dec.d, st.b3 / 3, ac, pk);
-  }
+  const uint32_t w = *(lds_cu32)(dec.tabs + (slot << 13) + ((pk >> (32 - kLookBits)) << 2));
+  uint32_t e = w & 0xFFFFu;
+  if (__builtin_expect((e & 31) == 0, 0)) e = lookup_long(dec, slot, e, pk, st.b3, ac);
   return e;
 }
 
@@ -235,31 +247,27 @@ __device__ __forceinline__ void advance(St &st, const Dec &dec, int adv) {
   st.k = end ? 0 : k2;
 }
 
-// Count-only step (blocks started) on the count-mode entries (HuffTab.cnt,
-// see ldt_types.hpp): one lookup consumes a run of AC symbols of one block
-// when k + PRE < 64, else the first symbol alone.
+// Count-only step (blocks started) on the count-mode entries (HuffTab.lc
+// high half, see ldt_types.hpp): one lookup consumes a run of AC symbols of
+// one block. A run's symbols before its last advance k by at most 15, so with
+// k <= 48 no block ends inside it; from k = 49 on, the l1 entry (low half:
+// the first symbol alone) is used. Both halves keep total bits at 0-4 and the
+// coefficient advance at 9-15.
 template <class W>
 __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int &nblk) {
   const uint32_t pk = R.peek();
-  const bool ac = st.k != 0;
-  const uint32_t slot = __builtin_amdgcn_ubfe(ac ? dec.acseq : dec.dcseq, (uint32_t)st.b3, 3u);
-  const lds_cu16 tb = dec.tabs + slot * kTabStride;
-  const uint32_t w = ((const LDS_AS uint32_t *)tb)[pk >> (32 - kLookBits)];
-  const uint32_t c = w >> 16, e1 = w & 0xFFFFu;
-  // the run, or its first symbol alone when a block would end inside it
-  const bool ok = (uint32_t)st.k + (c >> 12) < 64;
-  uint32_t t = ok ? (c & 31) : (e1 & 31);
-  uint32_t adv = ok ? ((c >> 5) & 127) : (e1 >> 9);
-  if (__builtin_expect((e1 & 31) == 0, 0)) { // long code
-    uint32_t e;
-    if (e1 != kHuffCanon)
-      e = tb[kL2Off + ((e1 >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
-    else
-      e = lookup_canon(dec.g, dec.d, st.b3 / 3, ac, pk);
-    t = e & 31;
-    adv = e >> 9;
+  const bool dcs = st.k == 0;
+  const uint32_t slot = __builtin_amdgcn_ubfe(dcs ? dec.dcseq : dec.acseq, (uint32_t)st.b3, 3u);
+  const uint32_t w = *(lds_cu32)(dec.tabs + (slot << 13) + ((pk >> (32 - kLookBits)) << 2));
+  const uint32_t e = st.k >= 49 ? (w << 16) : w; // the entry in the high half
+  uint32_t t = __builtin_amdgcn_ubfe(e, 16u, 5u);
+  uint32_t adv = e >> 25;
+  if (__builtin_expect(t == 0, 0)) { // long code: the first symbol alone
+    const uint32_t e2 = lookup_long(dec, slot, w & 0xFFFFu, pk, st.b3, !dcs);
+    t = e2 & 31;
+    adv = e2 >> 9;
   }
-  nblk += st.k == 0 ? 1 : 0;
+  nblk += dcs ? 1 : 0;
   R.consume((int)t);
   advance(st, dec, (int)adv);
 }
@@ -352,7 +360,7 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
   if (status[img] != 0 || descs[img].nseg == 0 || descs[img].sub_bits > 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
-  const Dec dec = load_dec(d, htabs, (lds_u16)dyn_lds, tid, 64);
+  const Dec dec = load_dec(d, htabs, (LDS_AS uint8_t *)dyn_lds, tid, 64);
   __syncthreads();
   for (int si = d.seg_base + tid; si < d.seg_base + d.nseg; si += 64) {
     const Segment sg = segs[si];
@@ -882,7 +890,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   const int tid = threadIdx.x;
   const uint64_t t_start = wall_clock64();
   // dynamic LDS: [window win_bytes][tables]
-  const Dec dec = load_dec(d, htabs, (lds_u16)(dyn_lds + win_bytes / 4), tid, kHuffThreads);
+  const Dec dec = load_dec(d, htabs, (LDS_AS uint8_t *)(dyn_lds + win_bytes / 4), tid, kHuffThreads);
   for (int s = tid; s < d.nseg; s += kHuffThreads) {
     const Segment &sg = segs[d.seg_base + s];
     sh.seg_first[s] = sg.sub_first;

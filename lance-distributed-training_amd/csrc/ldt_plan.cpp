@@ -234,7 +234,7 @@ bool build_huff(const RawHuff &r, bool is_dc, HuffTab &t) {
       adv += e2 >> 9;
       T += t2;
     }
-    t.lc[x] = e | ((T | (adv << 5) | (pre << 12)) << 16);
+    t.lc[x] = e | ((T | (pre << 5) | (adv << 9)) << 16);
   }
   return true;
 }

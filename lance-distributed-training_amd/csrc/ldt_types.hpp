@@ -122,14 +122,15 @@ __host__ __device__ inline uint16_t huff_entry(int len, int sym, bool dc) {
   return (uint16_t)((len + s) | (s << 5) | (adv << 9));
 }
 // Count-mode entries (the parallel decoder's sync passes only count blocks,
-// so one lookup may consume several symbols), per kLookBits-bit peek:
+// so one lookup may consume several symbols), per kLookBits-bit peek, laid out
+// like the l1 entries (total bits 0-4, advance 9-15):
 //   T (bits 0-4)    bits of the longest run of AC symbols of one block whose
 //                   codes all lie in the peeked bits (the last symbol's
 //                   magnitude may extend past them); DC tables: one symbol
-//   ADV (5-11)      coefficient advance of the run (an EOB, 64, ends it)
-//   PRE (12-15)     advance before the run's last symbol (<= 15): the run is
-//                   valid only if k + PRE < 64 (no block ends inside it);
-//                   otherwise the l1 entry (first symbol alone) applies
+//   PRE (5-8)       advance before the run's last symbol (<= 15): no block
+//                   ends inside the run while k + PRE < 64 (the decoder uses
+//                   the run entries for k <= 48 only)
+//   ADV (9-15)      coefficient advance of the run (an EOB, 64, ends it)
 // T == 0: a long code; the entry equals l1's indirect entry.
 struct HuffTab {
   uint32_t lc[1 << kLookBits]; // l1 | cnt << 16
