@@ -46,8 +46,12 @@ namespace ldt {
 constexpr int kDsChunk = kDsChunkBytes;        // 16 bytes per lane
 constexpr int kDsWords = kDsChunk / 4 + 2;     // + the words before and after
 constexpr int kDsInLds = kDsWords + kDsWords / 8 + 1;
-// LDS output of one chunk: kept bytes + kSegPad per RSTn (2 input bytes each) + alignment
-constexpr int kDsOutLds = (kDsChunk + kSegPad * (kDsChunk / 2)) / 4 + 4;
+// LDS output of one chunk: kept bytes + kSegPad per RSTn + alignment. Sized for
+// kDsRstLds markers per chunk (the workgroup then fits beside a k_huff_image
+// workgroup of another batch); a chunk with more writes its bytes straight to
+// memory.
+constexpr int kDsRstLds = 64;
+constexpr int kDsOutLds = (kDsChunk + kSegPad * kDsRstLds) / 4 + 4;
 
 __device__ __forceinline__ int ds_skew(int w) { return w + (w >> 3); }
 
@@ -215,6 +219,23 @@ __global__ void __launch_bounds__(256) k_destuff_write(const uint8_t *__restrict
   const int gend = lo_b + ktot + kSegPad * rpads;
   int r = rb + rex;
   int o = lo_b + kex + kSegPad * (min(r, last) - min(rb, last));
+  uint8_t *out = dst + d.dst_off;
+  if (rtot > kDsRstLds) { // marker-dense chunk: bytes straight to memory
+    uint8_t *ob = out + gal;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (rst & (1u << j)) {
+        if (r < last) {
+          for (int q = 0; q < kSegPad; ++q) ob[o + q] = 0;
+          o += kSegPad;
+        }
+        ++r;
+        if (r < d.nseg) segs[d.seg_base + r].byte_start = d.dst_off + gal + o;
+      }
+      if (keep & (1u << j)) ob[o++] = (uint8_t)(wv[(j + 4) >> 2] >> (8 * ((j + 4) & 3)));
+    }
+    return;
+  }
   if (keep == 0xFFFFu) {
     // all 16 bytes kept, no marker: a byte-shifted copy of the input run
     const int a = o & 3, w0 = o >> 2;
@@ -243,7 +264,6 @@ __global__ void __launch_bounds__(256) k_destuff_write(const uint8_t *__restrict
     }
   }
   __syncthreads();
-  uint8_t *out = dst + d.dst_off;
   for (int w = tid; 4 * w < gend; w += 256) {
     const int b0 = 4 * w;
     if (b0 >= lo_b && b0 + 4 <= gend) {

@@ -315,6 +315,29 @@ def test_many_restart_segments_take_serial_decoder():
         _check(out[k], oracle.jpeg_to_tensor(b), f"restart-mix[{k}]")
 
 
+def test_marker_dense_chunks_destuff_direct():
+    """Destuff chunks holding more than 64 RSTn markers (a marker every block
+    of a small, low-quality image) write their bytes straight to memory instead
+    of through the LDS staging buffer; bit-exact vs the oracle next to a chunk
+    that takes the staged path."""
+    import numpy as np
+
+    import ldt_amd
+    from ldt_amd import synth
+
+    gray = synth.field(256, 256, 95, 2.0)[:, :, 0]
+    dense = synth.encode(np.ascontiguousarray(gray), quality=20, restart_marker_blocks=1)
+    color = synth.encode(synth.field(256, 320, 96, 2.0), quality=25, restart_marker_blocks=1)
+    # markers per 4 KB of scan data (the chunk size)
+    n_rst = sum(dense.count(bytes([0xFF, 0xD0 + i])) for i in range(8))
+    assert n_rst * 4096 / len(dense) > 64 * 4
+    c2, _ = synth.q90_512(1, seed=97)
+    cells = [dense, c2[0], color]
+    out = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+    for k, b in enumerate(cells):
+        _check(out[k], oracle.jpeg_to_tensor(b), f"marker-dense[{k}]")
+
+
 def test_large_image_streaming_fallback_and_too_large():
     """A 3000x2000 source exceeds the banded kernel's LDS budget and takes the
     streaming k_resize path; a 9000-wide image exceeds LDT_MAX_DIM."""
