@@ -627,9 +627,10 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     d.dst_off = dst_total;
     dst_total += destuff_region_bytes(d.src_len, d.nseg);
     } // !progressive
+    // each image's coefficients: eight group planes of npad blocks (coef_piece)
     d.coef_off = coef_blocks;
     const int64_t nblk = nmcu * d.bpm;
-    coef_blocks += nblk;
+    coef_blocks += (nblk + kCoefAlign - 1) & ~(int64_t)(kCoefAlign - 1);
     if (nblk > max_blocks) max_blocks = nblk;
     if (resize_fast420(d)) ++n_fast420;
     if (H.width > max_w) max_w = H.width;

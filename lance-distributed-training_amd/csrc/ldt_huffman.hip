@@ -7,8 +7,9 @@
 //         s == 0: r == 15 ? k += 15 (ZRL) : break (EOB)
 // Bits past a segment's end read as zero (jdhuff.c inserts zeros at a marker;
 // here k_destuff leaves kSegPad zero bytes after every segment).
-// Input: destuffed segments (k_destuff). Output: int16 coefficients, natural
-// order, block (mcu, b) at coef_off + mcu * bpm + b (raw, dequantised in k_idct).
+// Input: destuffed segments (k_destuff). Output: int16 coefficients in zigzag
+// order, image-relative block (mcu, b) = mcu * bpm + b in the image's group
+// planes (coef_piece; raw, dequantised in k_idct).
 //
 // The symbol step is uniform for DC and AC: a table entry carries the bits to
 // consume (code + magnitude), the magnitude width s and the advance of the
@@ -21,6 +22,7 @@
 //   k_huff_image     the self-synchronising parallel decoder (Weissenberger &
 //                    Schmidt, ICPP 2018), one 1024-lane workgroup per image.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -141,51 +143,87 @@ __device__ __forceinline__ St make_state(int bk) {
 
 // Distinct tables of an image's six contexts (2 * component + AC), first
 // come first slot; slotmap holds 3 bits per context.
+// Constant indices only (fully unrolled selects), so slot_tab stays in
+// registers instead of a scratch array.
 __device__ __forceinline__ int image_slots(const ImgDesc &d, uint32_t &slotmap, int *slot_tab) {
-  int ns = 0;
-  slotmap = 0;
+  int t[6], sl[6];
+#pragma unroll
   for (int x = 0; x < 6; ++x) {
     const int c = x >> 1;
     const int cc = c < d.ncomp ? c : 0;
-    const int tix = (x & 1) ? d.act[cc] : d.dct[cc];
+    t[x] = (x & 1) ? d.act[cc] : d.dct[cc];
+    slot_tab[x] = 0;
+  }
+  int ns = 0;
+  slotmap = 0;
+#pragma unroll
+  for (int x = 0; x < 6; ++x) {
     int found = -1;
-    for (int q = 0; q < ns; ++q)
-      if (slot_tab[q] == tix) found = q;
-    if (found < 0) {
-      found = ns;
-      slot_tab[ns++] = tix;
-    }
-    slotmap |= (uint32_t)found << (3 * x);
+#pragma unroll
+    for (int y = 0; y < x; ++y)
+      if (found < 0 && t[y] == t[x]) found = sl[y];
+    const bool fresh = found < 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      if (fresh && q == ns) slot_tab[q] = t[x];
+    sl[x] = fresh ? ns : found;
+    ns += fresh ? 1 : 0;
+    slotmap |= (uint32_t)sl[x] << (3 * x);
   }
   return ns;
 }
 
-// Copy an image's distinct tables into LDS and return the decode constants.
-// lc parts at an 8 KB stride (the slot's offset is one shift), l2 parts after
-// them.
+// An image's distinct tables in LDS: lc parts at an 8 KB stride (the slot's
+// offset is one shift), l2 parts after them. Piece i (16 bytes) of the copy:
+// its source in the plan tables and its LDS byte offset.
+constexpr int kTabPieces = (kLcBytes + kL2Bytes) / 16; // HuffTab: lc then l2
+typedef uint32_t v4u __attribute__((ext_vector_type(4))); // 16-byte piece (LDS-storable)
+static_assert(sizeof(HuffTab) % 16 == 0, "16-byte table pieces");
+__device__ __forceinline__ const v4u *tab_piece_src(const HuffTab *__restrict__ htabs,
+                                                      const int *slot_tab, int i, int &dst, int ns) {
+  const int q = i / kTabPieces, o = i - q * kTabPieces;
+  int tix = slot_tab[0];
+#pragma unroll
+  for (int x = 1; x < 6; ++x)
+    if (q == x) tix = slot_tab[x];
+  dst = o < kLcBytes / 16 ? (q << 13) + 16 * o : (ns << 13) + q * kL2Bytes + 16 * o - kLcBytes;
+  return reinterpret_cast<const v4u *>(htabs + tix) + o;
+}
+
+// The decode constants of an image; with `copy`, also its tables into LDS
+// (k_huff_image stages them itself, together with the stream window).
 __device__ __forceinline__ Dec load_dec(const ImgDesc &d, const HuffTab *__restrict__ htabs,
-                                        LDS_AS uint8_t *tabs, int tid, int nthreads) {
+                                        LDS_AS uint8_t *tabs, int tid, int nthreads,
+                                        bool copy = true, int *slot_tab_out = nullptr) {
   int slot_tab[6];
   uint32_t slotmap;
   const int ns = image_slots(d, slotmap, slot_tab);
-  constexpr int kWords = (kLcBytes + kL2Bytes) / 4; // HuffTab: lc then l2
-  for (int i = tid; i < ns * kWords; i += nthreads) {
-    const int q = i / kWords, o = i - q * kWords;
-    int tix = slot_tab[0];
+  if (copy) {
+    for (int i = tid; i < ns * kTabPieces; i += nthreads) {
+      int dst;
+      const v4u v = *tab_piece_src(htabs, slot_tab, i, dst, ns);
+      *(LDS_AS v4u *)(tabs + dst) = v;
+    }
+  }
+  if (slot_tab_out) {
 #pragma unroll
-    for (int x = 1; x < 6; ++x)
-      if (q == x) tix = slot_tab[x];
-    const uint32_t v = reinterpret_cast<const uint32_t *>(htabs + tix)[o];
-    const int dst = o < kLcBytes / 4 ? (q << 13) + 4 * o : (ns << 13) + q * kL2Bytes + 4 * o - kLcBytes;
-    *(LDS_AS uint32_t *)(tabs + dst) = v;
+    for (int x = 0; x < 6; ++x) slot_tab_out[x] = slot_tab[x];
   }
   Dec dec;
   dec.tabs = tabs;
   dec.dcseq = dec.acseq = 0;
-  for (int b = 0; b < d.bpm; ++b) {
-    const int c = d.bcomp[b] & 3;
-    dec.dcseq |= ((slotmap >> (6 * c)) & 7) << (3 * b);
-    dec.acseq |= ((slotmap >> (6 * c + 3)) & 7) << (3 * b);
+  // constant indices into dword loads of bcomp (4-aligned in ImgDesc): scalar
+  // loads of the descriptor, no loop of dependent byte loads
+  static_assert(offsetof(ImgDesc, bcomp) % 4 == 0, "bcomp dword loads");
+  const uint32_t *bcw = reinterpret_cast<const uint32_t *>(d.bcomp);
+  const uint32_t bw[3] = {bcw[0], bcw[1], bcw[2]};
+#pragma unroll
+  for (int b = 0; b < kMaxBlocksPerMcu; ++b) {
+    if (b < d.bpm) {
+      const int c = (int)(bw[b >> 2] >> (8 * (b & 3))) & 3;
+      dec.dcseq |= ((slotmap >> (6 * c)) & 7) << (3 * b);
+      dec.acseq |= ((slotmap >> (6 * c + 3)) & 7) << (3 * b);
+    }
   }
   dec.ns = ns;
   dec.acmask = 0;
@@ -279,22 +317,22 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
 // coefficient indices only grow, so a group is complete once the index leaves
 // it or the block ends. Groups a neighbouring range may also write (a block
 // straddling the range boundary) are written slot by slot.
-__device__ __forceinline__ void store_group(int16_t *__restrict__ p, uint64_t lo, uint64_t hi) {
-  *reinterpret_cast<uint4 *>(p) =
-      make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+__device__ __forceinline__ void store_group(uint4 *__restrict__ p, uint64_t lo, uint64_t hi) {
+  *p = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
 // Coefficient-writing decode of one range: from the reader's position until
 // it reaches `stop` or the segment's `total` blocks are complete. cursor is
 // the current block (segment-relative, -1 before the first DC). DC symbols
 // store their difference in dcv_seg[cursor] (k_dc_scan adds the predictors);
-// nonzero AC coefficients go to coef_seg, which is all zero beforehand
-// (k_idct clears every block it reads). The loop body is straight-line: every
+// nonzero AC coefficients go to the image's group planes (block
+// seg_blk0 + cursor of coef_img, see coef_piece), which are all zero
+// beforehand (k_idct clears every block it reads). The loop body is straight-line: every
 // store is predicated, so a wave branches only around stores no lane makes.
 template <class W>
 __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
-                                          int &cursor, int total, int16_t *__restrict__ coef_seg,
-                                          int16_t *__restrict__ dcv_seg) {
+                                          int &cursor, int total, uint4 *__restrict__ coef_img,
+                                          int seg_blk0, int npad, int16_t *__restrict__ dcv_seg) {
   uint64_t lo = 0, hi = 0; // buffered group: slots 0-3, 4-7
   int grp = -1;            // its index (slot >> 3), -1 = empty
   // entered mid-block: the previous range may have written this group of it
@@ -314,13 +352,14 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     const bool nz = !dc && ((e >> 5) & 15) != 0;
     const int slot = st.k + adv - 1;
     const int g = slot >> 3;
-    int16_t *__restrict__ blk = coef_seg + (int64_t)cursor * 64;
+    // the block's groups in the image's group planes (coef_piece)
+    const int ib = seg_blk0 + cursor;
     if (dc) dcv_seg[cursor] = (int16_t)v;
     const bool direct = nz && first && g == shared_g;
-    if (direct && inb) blk[slot] = (int16_t)v;
+    if (direct && inb) reinterpret_cast<int16_t *>(coef_img + coef_piece(ib, g, npad))[slot & 7] = (int16_t)v;
     const bool buf = nz && !direct;
     const bool newg = buf && g != grp;
-    if (newg && grp >= 0 && inb) store_group(blk + 8 * grp, lo, hi);
+    if (newg && grp >= 0 && inb) store_group(coef_img + coef_piece(ib, grp, npad), lo, hi);
     lo = newg ? 0ull : lo;
     hi = newg ? 0ull : hi;
     grp = newg ? g : grp;
@@ -329,14 +368,14 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     hi |= (slot & 4) ? x : 0ull;
     R.consume((int)(e & 31));
     const bool end = st.k + adv >= 64;
-    if (end && grp >= 0 && inb) store_group(blk + 8 * grp, lo, hi);
+    if (end && grp >= 0 && inb) store_group(coef_img + coef_piece(ib, grp, npad), lo, hi);
     grp = end ? -1 : grp;
     first = first && !end;
     advance(st, dec, adv);
     go = R.p < stop && !(st.k == 0 && cursor + 1 >= total);
   }
   if (grp >= 0 && (uint32_t)cursor < (uint32_t)total) { // the open block continues in the next range
-    int16_t *p = coef_seg + (int64_t)cursor * 64 + 8 * grp;
+    int16_t *p = reinterpret_cast<int16_t *>(coef_img + coef_piece(seg_blk0 + cursor, grp, npad));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint16_t x = (uint16_t)(((j & 4) ? hi : lo) >> (16 * (j & 3)));
@@ -372,9 +411,10 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
     St st = make_state(0);
     const int total = sg.mcu_count * d.bpm;
     int cursor = -1;
-    const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
+    const int blk0 = sg.mcu_first * d.bpm; // image-relative
     // a valid segment ends inside its bits; 64 bits of slack bound a corrupt one
-    write_run(R, st, dec, pbias + seg_bits + 64, cursor, total, coef + blk0 * 64, dcv + blk0);
+    write_run(R, st, dec, pbias + seg_bits + 64, cursor, total,
+              reinterpret_cast<uint4 *>(coef + d.coef_off * 64), blk0, coef_npad(d), dcv + d.coef_off + blk0);
     if (R.p - pbias > seg_bits || cursor + 1 < total || st.k != 0) status[img] = 3; // truncated
   }
 }
@@ -855,12 +895,13 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   if (live) {
     int cursor = pre - sh.ex_p[sh.seg_first[g.si]] - 1; // segment-relative block, -1 before the DC
     const int total = sg.mcu_count * d.bpm;
-    const int64_t blk0 = d.coef_off + (int64_t)sg.mcu_first * d.bpm;
+    const int blk0 = sg.mcu_first * d.bpm; // image-relative
     St st = make_state(wbk);
     Rd<W> R;
     R.src = src;
     R.seek(g.pbias + wp);
-    write_run(R, st, dec, wstop, cursor, total, coef + blk0 * 64, dcv + blk0);
+    write_run(R, st, dec, wstop, cursor, total, reinterpret_cast<uint4 *>(coef + d.coef_off * 64), blk0,
+              coef_npad(d), dcv + d.coef_off + blk0);
     if (g.j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
   }
   // diagnostic phase times (10 ns ticks summed over images; ldt_debug_counters)
@@ -890,7 +931,9 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   const int tid = threadIdx.x;
   const uint64_t t_start = wall_clock64();
   // dynamic LDS: [window win_bytes][tables]
-  const Dec dec = load_dec(d, htabs, (LDS_AS uint8_t *)(dyn_lds + win_bytes / 4), tid, kHuffThreads);
+  LDS_AS uint8_t *tabs = (LDS_AS uint8_t *)(dyn_lds + win_bytes / 4);
+  int slot_tab[6];
+  const Dec dec = load_dec(d, htabs, tabs, tid, kHuffThreads, false, slot_tab);
   for (int s = tid; s < d.nseg; s += kHuffThreads) {
     const Segment &sg = segs[d.seg_base + s];
     sh.seg_first[s] = sg.sub_first;
@@ -907,18 +950,47 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   const int64_t need = destuff_region_bytes(d.src_len, d.nseg) + 16;
   const bool in_lds = need <= win_bytes;
   const uint8_t *base = dstuf + d.dst_off; // 16-aligned
-  if (in_lds) {
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  {
+    // Tables and (when it fits) the whole destuffed stream, byte-swapped, into
+    // LDS, with all of a lane's 16-byte pieces in flight at once (a loop of
+    // single loads waits on each one: ~13 dependent round trips per image).
+    // Every load is unconditional (clamped indices) so that no branch merge
+    // makes the compiler wait for the loads before it.
+    constexpr int kWinPer = 8;
+    const int ns = dec.ns;
+    const int otab = min(tid, kTabPieces - 1);
+    v4u tv[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) // slot q's pieces on lanes 0..kTabPieces-1 (q is uniform)
+      tv[q] = reinterpret_cast<const v4u *>(htabs + slot_tab[q < ns ? q : 0])[otab];
     const v4u *gsrc = reinterpret_cast<const v4u *>(base);
     LDS_AS v4u *wl = (LDS_AS v4u *)dyn_lds;
-    for (int i = tid; i < (int)(need / 16); i += kHuffThreads) {
-      const v4u v = gsrc[i];
-      v4u o;
-      o.x = __builtin_bswap32(v.x);
-      o.y = __builtin_bswap32(v.y);
-      o.z = __builtin_bswap32(v.z);
-      o.w = __builtin_bswap32(v.w);
-      wl[i] = o;
+    const int nwin = in_lds ? (int)(need / 16) : 0;
+    for (int r0 = 0; r0 == 0 || r0 < nwin; r0 += kWinPer * kHuffThreads) {
+      v4u v[kWinPer];
+#pragma unroll
+      for (int k = 0; k < kWinPer; ++k) v[k] = gsrc[max(min(r0 + k * kHuffThreads + tid, nwin - 1), 0)];
+      if (r0 == 0 && tid < kTabPieces) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          if (q < ns) {
+            const int dst = tid < kLcBytes / 16 ? (q << 13) + 16 * tid : (ns << 13) + q * kL2Bytes + 16 * tid - kLcBytes;
+            *(LDS_AS v4u *)(tabs + dst) = tv[q];
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kWinPer; ++k) {
+        const int i = r0 + k * kHuffThreads + tid;
+        if (i < nwin) {
+          v4u o;
+          o.x = __builtin_bswap32(v[k].x);
+          o.y = __builtin_bswap32(v[k].y);
+          o.z = __builtin_bswap32(v[k].z);
+          o.w = __builtin_bswap32(v[k].w);
+          wl[i] = o;
+        }
+      }
     }
   }
   __syncthreads();

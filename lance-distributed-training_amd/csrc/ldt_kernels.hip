@@ -438,8 +438,9 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
 // One lane per 8x8 block: the whole block stays in registers for both
 // passes (no transposes, no barriers between them). A workgroup covers
 // kIdctBlocksPerWg consecutive blocks of one image; each lane loads its
-// block's 128-B line straight into registers (no LDS tile: occupancy is set by
-// registers alone, so more blocks are in flight).
+// block's eight 16-B groups straight into registers (no LDS tile: occupancy is
+// set by registers alone, so more blocks are in flight). The group-plane
+// layout (coef_piece) makes each group load a contiguous 1 KB per wave.
 //
 // Coefficient buffer contract (with the Huffman decoders and k_prog): all
 // zero between batches. The Huffman pass writes only nonzero AC coefficient
@@ -477,13 +478,16 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
   // the lane's block straight into registers (one 128-B line per lane), and
   // zeros back over the groups that held coefficients (the all-zero
   // invariant; a failed image's blocks are cleared too)
-  uint4 *src = reinterpret_cast<uint4 *>(coef + (d.coef_off + blk) * 64);
+  // Group planes (coef_piece): group r of the wave's 64 consecutive blocks is
+  // one contiguous 1 KB, so each of the 8 loads and zero stores is coalesced.
+  uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
+  const int npad = coef_npad(d);
   uint4 raw[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) raw[r] = src[r];
+  for (int r = 0; r < 8; ++r) raw[r] = cimg[coef_piece((int)blk, r, npad)];
 #pragma unroll
   for (int r = 0; r < 8; ++r)
-    if ((raw[r].x | raw[r].y | raw[r].z | raw[r].w) != 0) src[r] = make_uint4(0u, 0u, 0u, 0u);
+    if ((raw[r].x | raw[r].y | raw[r].z | raw[r].w) != 0) cimg[coef_piece((int)blk, r, npad)] = make_uint4(0u, 0u, 0u, 0u);
   if (!ok) return;
   const int64_t m = blk / d.bpm;
   const int b = (int)(blk - m * d.bpm);

@@ -48,11 +48,29 @@ struct DevPlan {
   const int32_t *chunk_img; // chunk -> image
 };
 
+// Coefficient buffer layout, per image: eight group planes. Zigzag slots
+// 8g..8g+7 of image-relative block ib (a 16-byte piece) sit at piece
+// g * npad + ib of the image's region (npad = its block count rounded up to
+// 64; regions start at coef_off * 64 int16s, coef_off % 64 == 0). The 64 lanes
+// of a wave that own 64 consecutive blocks then read or clear group g of all
+// of them with one contiguous 1 KB access (k_idct), while the Huffman write
+// pass still stores whole 16-byte groups at one multiply-add per address.
+constexpr int kCoefAlign = 64;
+__host__ __device__ __forceinline__ int coef_npad(const ImgDesc &d) {
+  return (int)(((int64_t)d.mcux * d.mcuy * d.bpm + kCoefAlign - 1) & ~(int64_t)(kCoefAlign - 1));
+}
+// Index of the 16-byte piece (block ib, group g) from the image's region start.
+// npad < 2^24 (LDT_MAX_DIM 8192, 4:4:4), so this is one 24-bit multiply-add.
+__host__ __device__ __forceinline__ uint32_t coef_piece(int ib, int g, int npad) {
+  return __umul24((unsigned)g, (unsigned)npad) + (unsigned)ib;
+}
+
 struct DevWork {
   const uint8_t *data;  // compressed cells
   uint8_t *dstuf;       // destuffed entropy data
-  int16_t *coef;        // AC coefficients (the DC slot of each block is unused); all zero
-                        // between batches (k_idct clears every block it reads)
+  int16_t *coef;        // AC coefficients (the DC slot of each block is unused), in
+                        // group planes (coef_piece); all zero between batches (k_idct
+                        // clears every block it reads)
   int16_t *dcv;         // per block: DC difference (Huffman), then absolute DC (k_dc_scan)
   uint8_t *planes;      // component planes
   int32_t *status;      // per image

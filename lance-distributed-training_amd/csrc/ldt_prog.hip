@@ -346,12 +346,11 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
         if (dcband) {
           L.dc[lane] = dcv[gb];
         } else {
-          const int4 *src = reinterpret_cast<const int4 *>(coef + gb * 64);
           int4 *dst = reinterpret_cast<int4 *>(L.blk[lane]);
           uint64_t nz = 0;
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const int4 v = src[q];
+            const int4 v = reinterpret_cast<const int4 *>(coef + d.coef_off * 64)[coef_piece((int)blk, q, coef_npad(d))];
             dst[q] = v;
             const uint32_t w[4] = {(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w};
 #pragma unroll
@@ -469,10 +468,10 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
         if (dcband) {
           dcv[gb] = L.dc[lane];
         } else {
-          int4 *dst = reinterpret_cast<int4 *>(coef + gb * 64);
           const int4 *src = reinterpret_cast<const int4 *>(L.blk[lane]);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) dst[q] = src[q];
+          for (int q = 0; q < 8; ++q)
+            reinterpret_cast<int4 *>(coef + d.coef_off * 64)[coef_piece((int)(gb - d.coef_off), q, coef_npad(d))] = src[q];
         }
       }
       if (piped) { // publish chunk ci once the wave's stores are done
