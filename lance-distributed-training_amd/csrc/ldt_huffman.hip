@@ -350,7 +350,10 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     const int v = ext_value(pk, e);
     const int adv = (int)(e >> 9);
     const bool nz = !dc && ((e >> 5) & 15) != 0;
-    const int slot = st.k + adv - 1;
+    // a corrupt stream can run k past 63 (a run or ZRL from k > 48): jdhuff.c
+    // then stores into natural[k >= 64] = position 63; so does this clamp
+    // (and it keeps the store inside the block's eight groups)
+    const int slot = min(st.k + adv - 1, 63);
     const int g = slot >> 3;
     // the block's groups in the image's group planes (coef_piece)
     const int ib = seg_blk0 + cursor;
