@@ -261,9 +261,11 @@ __device__ __forceinline__ uint32_t lookup_long(const Dec &dec, uint32_t slot, u
 __device__ __forceinline__ uint32_t lookup(const Dec &dec, const St &st, uint32_t pk) {
   const bool ac = st.k != 0;
   const uint32_t slot = __builtin_amdgcn_ubfe(ac ? dec.acseq : dec.dcseq, (uint32_t)st.b3, 3u);
-  const uint32_t w = *(lds_cu32)(dec.tabs + (slot << 13) + ((pk >> (32 - kLookBits)) << 2));
-  uint32_t e = w & 0xFFFFu;
-  if (__builtin_expect((e & 31) == 0, 0)) e = lookup_long(dec, slot, e, pk, st.b3, ac);
+  // the l1 entry: the low 16-bit half of the lc word, read on its own
+  uint32_t e = *(lds_cu16)(dec.tabs + (slot << 13) + ((pk >> (32 - kLookBits)) << 2));
+  // long codes are rare: a wave-uniform test keeps the exec mask untouched
+  if (__builtin_expect(__any((e & 31) == 0), 0))
+    if ((e & 31) == 0) e = lookup_long(dec, slot, e, pk, st.b3, ac);
   return e;
 }
 
@@ -296,14 +298,21 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
   const uint32_t pk = R.peek();
   const bool dcs = st.k == 0;
   const uint32_t slot = __builtin_amdgcn_ubfe(dcs ? dec.dcseq : dec.acseq, (uint32_t)st.b3, 3u);
-  const uint32_t w = *(lds_cu32)(dec.tabs + (slot << 13) + ((pk >> (32 - kLookBits)) << 2));
-  const uint32_t e = st.k >= 49 ? (w << 16) : w; // the entry in the high half
-  uint32_t t = __builtin_amdgcn_ubfe(e, 16u, 5u);
-  uint32_t adv = e >> 25;
-  if (__builtin_expect(t == 0, 0)) { // long code: the first symbol alone
-    const uint32_t e2 = lookup_long(dec, slot, w & 0xFFFFu, pk, st.b3, !dcs);
-    t = e2 & 31;
-    adv = e2 >> 9;
+  // the entry's 16-bit half straight from LDS (no shift/select after the
+  // load, which is on the bit-position dependency chain): the count-mode
+  // half (high) while k <= 48, the l1 half (low) from k = 49
+  // (table offset and half come from the state, off the chain: one add3)
+  const uint32_t soff = (slot << 13) + (st.k >= 49 ? 0u : 2u);
+  const uint32_t idx4 = (pk >> (32 - kLookBits)) << 2;
+  const uint32_t e = *(lds_cu16)(dec.tabs + soff + idx4);
+  uint32_t t = e & 31u;
+  uint32_t adv = e >> 9;
+  if (__builtin_expect(__any(t == 0), 0)) {
+    if (t == 0) { // long code: the first symbol alone
+      const uint32_t e2 = lookup_long(dec, slot, *(lds_cu16)(dec.tabs + (slot << 13) + idx4), pk, st.b3, !dcs);
+      t = e2 & 31;
+      adv = e2 >> 9;
+    }
   }
   nblk += dcs ? 1 : 0;
   R.consume((int)t);
