@@ -295,6 +295,9 @@ def main():
         standalone = solo.stage_times(reset=True)
         solo.check()
 
+    # measured HBM ceiling on this box, after the timed region
+    ceiling = stream_copy_ceiling(dev)
+
     # roofline: the resize/normalise stage (north_star), from live HIP events
     rs_ms, rs_n = stages["resize"]
     rs_avg_s = rs_ms / max(rs_n, 1) / 1e3
@@ -343,6 +346,11 @@ def main():
             "frac": round(sa_ach / HBM_PEAK_GBS, 4),
             "timing": "HIP events, one batch in flight (4 batches after the timed region)"}
         res["stages_standalone_ms"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in standalone.items()}
+        res["roofline"]["standalone"]["frac_of_measured"] = round(sa_ach / ceiling, 4)
+    res["roofline"]["measured_ceiling"] = {
+        "stream_copy_gbs": round(ceiling, 1), "frac_of_measured": round(achieved / ceiling, 4),
+        "method": "device-to-device copy of 1 GiB (read + write counted), torch's vectorised copy kernel, "
+                  "best of 10, HIP events; measured after the timed region"}
     tr = load_profile(f"traffic_{args.workload}.json")
     if tr is not None and tr.get("batch", B) == B:
         res["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
@@ -372,6 +380,28 @@ def main():
 
 
 PROFILE_ROUND = "r2"
+
+
+def stream_copy_ceiling(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
+    """Measured HBM stream ceiling in GB/s: 2 * nbytes per device-to-device copy."""
+    import torch
+
+    a = torch.full((nbytes // 4,), 1.0, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    best = 0.0
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = max(best, 2.0 * nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9)
+    del a, b
+    torch.cuda.empty_cache()
+    return best
 
 
 def load_profile(name: str):
