@@ -1,0 +1,44 @@
+"""bench.py keeps the driver's contract: one JSON line on stdout with the
+required keys, roofline and measured-ceiling objects, for the headline (c2)
+and the raw HBM-stress (c5) workloads. Small step counts; no CPU legs."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config", "roofline")
+
+
+def _bench(*args):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["c2", "c5"])
+def test_bench_json_contract(workload):
+    d = _bench("--workload", workload, "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    for k in REQUIRED:
+        assert k in d, k
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        assert d["metric"] == json.load(f)["metric"]
+    assert d["unit"] == "img/s" and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["value"] > 0
+    assert d["vs_baseline"] is None  # BASELINE.md publishes no number for this metric
+    assert "workload" in d["config"] and d["config"]["workload"].startswith(workload)
+    roof = d["roofline"]
+    assert roof["bound"] == "hbm" and roof["unit"] == "GB/s" and roof["peak"] == 8000.0
+    assert 0 < roof["frac"] < 1 and abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
+    ceil = roof["measured_ceiling"]
+    assert 1000 < ceil["stream_copy_gbs"] < 8000
+    if workload == "c2":
+        assert d["dtype"] == "u8" and "standalone" in roof and "value_host_input" in d
+        assert set(d["stages_ms_per_step"]) >= {"destuff", "huffman", "idct", "resize"}
