@@ -785,15 +785,27 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     // trajectory adopts that trajectory again (exits flip between two values
     // while an unsynchronised stretch converges); repeated until no slot
     // changes, so a run of such slots resolves without decoding.
+    // The same reads give this round's needy slots once no slot adopts any
+    // more: the last pass of the loop leaves `need` and the per-wave counts
+    // of the work list behind (one barrier instead of a second pass).
+    bool need;
+    uint64_t bal;
     for (;;) {
       bool hit = false;
+      need = false;
       if (live && g.j > 0) {
         const int rel = sh.ex_p[tid - 1] - g.j * S;
         const int pbk = sh.ex_bk[tid - 1];
-        hit = (rel != (int)sh.en_p[tid] || pbk != (int)sh.en_bk[tid]) && rel == (int)sh.m_en_p[tid] &&
-              pbk == (int)sh.m_en_bk[tid];
+        need = rel != (int)sh.en_p[tid] || pbk != (int)sh.en_bk[tid];
+        hit = need && rel == (int)sh.m_en_p[tid] && pbk == (int)sh.m_en_bk[tid];
       }
-      __syncthreads(); // every read of the exits is done
+      bal = __ballot(need);
+      const uint64_t hbal = __ballot(hit);
+      if (lane == 0) {
+        sh.scan[wave] = __popcll(bal);
+        if (hbal) atomicAdd(&sh.memo_hits, __popcll(hbal));
+      }
+      if (!__syncthreads_or(hit)) break; // also: every read of the exits is done
       if (hit) {
         const uint16_t ep = sh.en_p[tid], ebk = sh.en_bk[tid], nb = sh.nblk[tid], xbk = sh.ex_bk[tid];
         const int xp = sh.ex_p[tid];
@@ -808,15 +820,9 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
         sh.m_ex_bk[tid] = xbk;
         sh.m_nblk[tid] = nb;
         sh.cp_n[tid] = 0; // the adopted trajectory's checkpoints are not kept
-        atomicAdd(&sh.memo_hits, 1);
       }
-      if (!__syncthreads_or(hit)) break;
+      __syncthreads(); // adoptions published
     }
-    const bool need = live && g.j > 0 &&
-                      (sh.ex_p[tid - 1] != (int)sh.en_p[tid] + g.j * S || sh.ex_bk[tid - 1] != sh.en_bk[tid]);
-    const uint64_t bal = __ballot(need);
-    if (lane == 0) sh.scan[wave] = __popcll(bal);
-    __syncthreads();
     int base = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < kHuffThreads / 64; ++w) {
