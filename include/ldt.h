@@ -133,6 +133,18 @@ int ldt_decode_batch_resident(ldt_ctx *ctx, const uint8_t *data_host, const uint
                               const ldt_norm *norm_or_null, void *stream,
                               int32_t *per_image_status);
 
+/* Zero-copy host input. ldt_register_host page-locks [ptr, ptr+len) in place
+ * (hipHostRegister) for every context of the process: a later ldt_decode_batch
+ * whose cells lie inside a registered range copies them to HBM by DMA straight
+ * from those pages, without the memcpy into the context's pinned ring. Meant
+ * for a memory-mapped Arrow IPC / Lance fragment registered once (the
+ * dataset's `image` data buffer), replacing the per-batch copy SURVEY.md
+ * §8f row 1 names. The range must stay mapped until ldt_unregister_host(ptr),
+ * which waits for the device first. Returns LDT_OK or LDT_ERR_* (a range the
+ * driver cannot lock stays on the copying path). */
+int ldt_register_host(ldt_ctx *ctx, const void *ptr, size_t len);
+int ldt_unregister_host(ldt_ctx *ctx, const void *ptr);
+
 /* Wait for the last decode on `stream` and merge device-side per-image errors
  * into per_image_status[n] (for LDT_OPT_SYNC_STATUS = 0). */
 int ldt_fetch_status(ldt_ctx *ctx, void *stream, int32_t *per_image_status, int64_t n);

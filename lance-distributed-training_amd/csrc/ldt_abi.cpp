@@ -241,6 +241,21 @@ int ensure_dev(ldt_ctx *c, DevBuf &b, size_t need, hipStream_t s, bool zero = fa
   return LDT_OK;
 }
 
+// Host ranges page-locked in place (ldt_register_host), for all contexts.
+struct HostRange {
+  uintptr_t lo, hi;
+};
+std::mutex g_host_m;
+std::vector<HostRange> g_host_ranges;
+
+bool host_registered(const void *p, size_t n) {
+  const uintptr_t lo = (uintptr_t)p, hi = lo + n;
+  std::lock_guard<std::mutex> l(g_host_m);
+  for (const HostRange &r : g_host_ranges)
+    if (lo >= r.lo && hi <= r.hi) return true;
+  return false;
+}
+
 void pinned_copy(ldt_ctx *c, void *dst, const void *src, size_t n) {
   if (!c->copier) {
     unsigned hw = std::thread::hardware_concurrency();
@@ -726,11 +741,16 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   tick(8, t0);
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
-    if ((rc = ensure_pin(c, c->h_data[sl], (size_t)total_bytes + 16))) return rc;
     if ((rc = ensure_dev(c, c->d_data, (size_t)total_bytes + 16, s))) return rc;
-    pinned_copy(c, c->h_data[sl].p, cells_host, (size_t)total_bytes);
-    HIPCHK(c, hipMemcpyAsync(c->d_data.p, c->h_data[sl].p, (size_t)total_bytes,
-                             hipMemcpyHostToDevice, s));
+    if (total_bytes > 0 && host_registered(cells_host, (size_t)total_bytes)) {
+      // page-locked in place: DMA straight from the caller's pages
+      HIPCHK(c, hipMemcpyAsync(c->d_data.p, cells_host, (size_t)total_bytes, hipMemcpyHostToDevice, s));
+    } else {
+      if ((rc = ensure_pin(c, c->h_data[sl], (size_t)total_bytes + 16))) return rc;
+      pinned_copy(c, c->h_data[sl].p, cells_host, (size_t)total_bytes);
+      HIPCHK(c, hipMemcpyAsync(c->d_data.p, c->h_data[sl].p, (size_t)total_bytes,
+                               hipMemcpyHostToDevice, s));
+    }
     dev_cells = static_cast<const uint8_t *>(c->d_data.p);
   }
   tick(6, t0);
@@ -886,6 +906,39 @@ void ldt_destroy(ldt_ctx *c) {
 }
 
 const char *ldt_last_error(ldt_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int ldt_register_host(ldt_ctx *c, const void *ptr, size_t len) {
+  if (!c || !ptr || len == 0) return c ? set_err(c, LDT_ERR_ARG, "register: empty range") : LDT_ERR_ARG;
+  DeviceGuard g(c->device);
+  if (host_registered(ptr, len)) return LDT_OK;
+  hipError_t e = hipHostRegister(const_cast<void *>(ptr), len, hipHostRegisterDefault);
+  if (e != hipSuccess) { // e.g. a read-only mapping
+    (void)hipGetLastError();
+    e = hipHostRegister(const_cast<void *>(ptr), len, hipHostRegisterReadOnly);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(c, LDT_ERR_HIP, "hipHostRegister(%zu bytes): %s", len, hipGetErrorString(e));
+  }
+  std::lock_guard<std::mutex> l(g_host_m);
+  g_host_ranges.push_back({(uintptr_t)ptr, (uintptr_t)ptr + len});
+  return LDT_OK;
+}
+
+int ldt_unregister_host(ldt_ctx *c, const void *ptr) {
+  if (!c) return LDT_ERR_ARG;
+  DeviceGuard g(c->device);
+  {
+    std::lock_guard<std::mutex> l(g_host_m);
+    auto it = std::find_if(g_host_ranges.begin(), g_host_ranges.end(),
+                           [&](const HostRange &r) { return r.lo == (uintptr_t)ptr; });
+    if (it == g_host_ranges.end()) return set_err(c, LDT_ERR_ARG, "unregister: range not registered");
+    g_host_ranges.erase(it);
+  }
+  HIPCHK(c, hipDeviceSynchronize()); // no copy from the range is still in flight
+  HIPCHK(c, hipHostUnregister(const_cast<void *>(ptr)));
+  return LDT_OK;
+}
 
 int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
   if (!c) return LDT_ERR_ARG;

@@ -14,6 +14,6 @@ from .dataset import (ArrowDataset, LanceDataset, SafeLanceDataset, dataset,  # 
 from .sampler import DistributedSampler, FullScanSampler, ShardedBatchSampler, ShardedFragmentSampler  # noqa: F401
 from .transforms import (IMAGENET_MEAN, IMAGENET_STD, DecodePipeline, ResidentBatch, collate_fn,  # noqa: F401
                          decode_arrow, decode_tensor_image, make_collate_fn, make_to_tensor_fn,
-                         resize_raw)
+                         register_host, resize_raw, unregister_host)
 
 __version__ = "0.1.0"

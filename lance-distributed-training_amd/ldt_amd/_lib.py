@@ -50,7 +50,7 @@ STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
 EXPORTED = (
     "ldt_create", "ldt_destroy", "ldt_last_error", "ldt_set_option", "ldt_version",
     "ldt_decode_batch", "ldt_decode_batch_large", "ldt_decode_batch_resident",
-    "ldt_fetch_status", "ldt_stage_times", "ldt_resize_raw", "ldt_shard_ranges",
+    "ldt_register_host", "ldt_unregister_host", "ldt_fetch_status", "ldt_stage_times", "ldt_resize_raw", "ldt_shard_ranges",
     "ldt_shard_fragments", "ldt_distributed_indices",
 )
 
@@ -123,7 +123,10 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
                                               vp, vp]
         L.ldt_debug_resample_coeffs.argtypes = [vp, i32, i32, vp, vp, vp]
         L.ldt_debug_counters.argtypes = [vp, vp, vp]
-        for name in ("ldt_set_option", "ldt_decode_batch", "ldt_decode_batch_large",
+        L.ldt_register_host.argtypes = [vp, vp, sz]
+        L.ldt_unregister_host.argtypes = [vp, vp]
+        for name in ("ldt_set_option", "ldt_decode_batch", "ldt_decode_batch_large", "ldt_register_host",
+                     "ldt_unregister_host",
                      "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_resize_raw", "ldt_stage_times",
                      "ldt_shard_ranges", "ldt_shard_fragments", "ldt_distributed_indices",
                      "ldt_debug_resample_coeffs",

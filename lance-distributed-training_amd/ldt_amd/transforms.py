@@ -428,6 +428,53 @@ def resize_raw(hwc, height: int, width: int, *, device=None, normalize=True):
     return out
 
 
+def _host_range(obj):
+    """(address, size) of the host bytes behind a pa.Buffer, the data buffer of
+    a binary/large_binary/fixed_size_binary pa.Array / ChunkedArray chunk, or
+    a numpy array."""
+    if isinstance(obj, pa.ChunkedArray):
+        if obj.num_chunks != 1:
+            raise ValueError("register one chunk at a time")
+        obj = obj.chunk(0)
+    if isinstance(obj, pa.Array):
+        bufs = obj.buffers()
+        obj = bufs[1] if pa.types.is_fixed_size_binary(obj.type) else bufs[2]
+    if isinstance(obj, pa.Buffer):
+        return obj.address, obj.size
+    if isinstance(obj, np.ndarray):
+        return obj.ctypes.data, obj.nbytes
+    raise TypeError(f"cannot register {type(obj).__name__}")
+
+
+_registered: dict = {}
+
+
+def register_host(obj, device=None):
+    """Page-lock the host bytes of `obj` in place (ldt_register_host), so that
+    every later decode of cells inside them copies to HBM by DMA without the
+    memcpy into the pinned ring: for a memory-mapped Arrow IPC / Lance
+    fragment, register the `image` column's data buffer once. The bytes must
+    stay alive until unregister_host(obj). Returns the registered (address,
+    size)."""
+    addr, size = _host_range(obj)
+    if size == 0 or addr in _registered:
+        return addr, size
+    dec = _decoder(device)
+    dec.ctx.check(dec.ctx.lib.ldt_register_host(dec.ctx.handle, addr, size), "ldt_register_host")
+    _registered[addr] = (size, obj, dec)  # keeps `obj` alive while registered
+    return addr, size
+
+
+def unregister_host(obj):
+    """Undo register_host (waits for the device first)."""
+    addr, _ = _host_range(obj)
+    ent = _registered.pop(addr, None)
+    if ent is None:
+        return
+    dec = ent[2]
+    dec.ctx.check(dec.ctx.lib.ldt_unregister_host(dec.ctx.handle, addr), "ldt_unregister_host")
+
+
 class ResidentBatch:
     """A batch of JPEG cells staged once into HBM (bench / pre-staged loaders).
 
@@ -611,7 +658,8 @@ class DecodePipeline:
             raise ImageDecodeError(bad)
 
 
-def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int = 0, **fixed):
+def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int = 0,
+                      register: bool = False, **fixed):
     """A pipelined ``to_tensor_fn`` for ``LanceDataset(..., to_tensor_fn=...)``
     (lance_iterable.py:53-59): each call enqueues its RecordBatch on one of
     `depth` contexts/streams and returns at once, so batch k+1's host copy and
@@ -622,10 +670,22 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
 
     ``prefetch=k`` (k < depth): ``LanceDataset`` iterates through
     ``fn.iterate`` instead, enqueueing the next k batches before yielding each
-    one, so their decode overlaps the consumer's training step."""
+    one, so their decode overlaps the consumer's training step.
+
+    ``register=True``: the first batch seen from each underlying `image` data
+    buffer page-locks that whole buffer in place (``register_host``), so the
+    batches sliced from a memory-mapped fragment reach HBM by DMA without a
+    host memcpy. Only for long-lived buffers (a mapped dataset), not for
+    batches built anew each step."""
     pipe = DecodePipeline(depth=depth, device=device)
+    image_column = fixed.get("image_column", "image")
+
+    def maybe_register(batch, col):
+        if register and isinstance(batch, pa.RecordBatch):
+            register_host(_column(batch, col), device=device)
 
     def to_tensor_fn(batch, **kwargs):
+        maybe_register(batch, kwargs.get("image_column", image_column))
         if pipe.k >= pipe.depth:
             pipe.check_slot(pipe.k % pipe.depth)
         img, lbl = pipe.decode(batch, normalize=kwargs.get("normalize", normalize),
@@ -636,7 +696,12 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
     to_tensor_fn.check = pipe.check
     to_tensor_fn.pipeline = pipe
     to_tensor_fn.prefetch = max(0, min(int(prefetch), depth - 1))
+    def registered(batches):
+        for b in batches:
+            maybe_register(b, image_column)
+            yield b
+
     to_tensor_fn.iterate = lambda batches: pipe.prefetch(
-        batches, ahead=to_tensor_fn.prefetch, normalize=normalize,
+        registered(batches), ahead=to_tensor_fn.prefetch, normalize=normalize,
         image_column=fixed.get("image_column", "image"), label_column=fixed.get("label_column", "label"))
     return to_tensor_fn

@@ -443,6 +443,44 @@ def test_pipelined_to_tensor_fn_host_batches():
     assert set(ei.value.rows) == {1}
 
 
+def test_registered_host_buffer_bit_exact():
+    """register_host (ldt_register_host): the image column's data buffer
+    page-locked in place; decodes of the whole batch and of slices inside it
+    take the DMA branch and are bit-exact with the unregistered path and the
+    oracle; make_to_tensor_fn(register=True) registers on first sight;
+    unregister_host restores the copy path."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import synth
+
+    cells, labels = synth.food101_like(24, seed=77)
+    rb = _batch(cells, labels)
+    ref = ldt_amd.decode_tensor_image(rb)["image"].cpu().numpy()
+    col = rb.column(0)
+    addr, size = ldt_amd.register_host(col)
+    try:
+        assert size == sum(len(c) for c in cells) and addr != 0
+        assert ldt_amd.register_host(col) == (addr, size)  # idempotent
+        got = ldt_amd.decode_tensor_image(rb)
+        assert np.array_equal(got["label"].cpu().numpy(), labels)
+        assert np.array_equal(got["image"].cpu().numpy(), ref)
+        part = ldt_amd.decode_tensor_image(rb.slice(5, 11))["image"].cpu().numpy()
+        assert np.array_equal(part, ref[5:16])
+        fn = ldt_amd.make_to_tensor_fn(depth=2, register=True)
+        outs = [fn(rb.slice(8 * k, 8)) for k in range(3)]
+        fn.check()
+        torch.cuda.synchronize()
+        for k, o in enumerate(outs):
+            assert np.array_equal(o["image"].cpu().numpy(), ref[8 * k:8 * k + 8])
+        for k in (0, 13, 23):
+            _check(ref[k], oracle.jpeg_to_tensor(cells[k]), "registered")
+    finally:
+        ldt_amd.unregister_host(col)
+    again = ldt_amd.decode_tensor_image(rb)["image"].cpu().numpy()
+    assert np.array_equal(again, ref)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_progressive_mixed_batches_vs_oracle(seed):
     """SOF2 images (k_prog: jdphuff.c scans) mixed with baseline ones in one
