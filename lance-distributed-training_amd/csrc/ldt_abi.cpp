@@ -816,13 +816,14 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   HIPCHK(c, launch_idct(p, w, s));
   prof_mark(c, LDT_STAGE_IDCT, s);
   {
+    // k_resize4 writes the failed images itself; the streaming fallback does not
     hipError_t rerr = hipSuccess;
-    if (!(c->resize_impl != 2 &&
-          launch_resize4_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr)))
-      rerr = launch_resize_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s);
+    const bool r4 = c->resize_impl != 2 &&
+                    launch_resize4_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr);
+    if (!r4) rerr = launch_resize_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s);
     HIPCHK(c, rerr);
+    if (!r4) HIPCHK(c, launch_fill_failed(p, w, out_img, labels ? out_lbl : nullptr, s));
   }
-  HIPCHK(c, launch_fill_failed(p, w, out_img, labels ? out_lbl : nullptr, s));
   prof_mark(c, LDT_STAGE_RESIZE, s);
   c->cur_ev = nullptr;
 

@@ -440,28 +440,23 @@ hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s)
 }
 
 // ---------------------------------------------------------------------------
-// k_dc_scan: DC predictors (jdhuff.c: last_dc_val[ci] += diff, reset to 0 at
-// every restart marker, process_restart). One workgroup per image; thread t
-// owns a run of consecutive blocks; a segmented scan over the threads carries
-// the per-component sums. Stores the absolute DC (JCOEF, truncated) in place.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ descs,
-                                                 int16_t *__restrict__ dcv,
-                                                 const int32_t *__restrict__ status) {
-  __shared__ int s_f[256];
-  __shared__ int s_v[3][256];
-  const int img = blockIdx.x;
-  if (status[img] != 0 || descs[img].nseg == 0) return; // progressive: dcv holds final DC
-  const ImgDesc &d = descs[img];
+// DC predictors (jdhuff.c: last_dc_val[ci] += diff, reset to 0 at every
+// restart marker, process_restart) of one image, by its NT-thread workgroup:
+// thread t owns a run of consecutive blocks; a segmented scan over the threads
+// carries the per-component sums. Stores the absolute DC (JCOEF, truncated) in
+// place. `scr` is 4*NT/64 ints of LDS; contains __syncthreads.
+template <int NT>
+__device__ __forceinline__ void dc_scan_image(const ImgDesc &d, int16_t *__restrict__ v,
+                                              LDS_AS int32_t *scr) {
+  static_assert(NT % 64 == 0, "whole waves");
   const int tid = threadIdx.x;
   const int bpm = d.bpm;
   const int64_t nblk = (int64_t)d.mcux * d.mcuy * bpm;
   const int64_t seglen = d.restart ? (int64_t)d.restart * bpm : nblk;
   uint32_t compmap = 0;
   for (int b = 0; b < bpm; ++b) compmap |= (uint32_t)(d.bcomp[b] & 3) << (2 * b);
-  const int64_t K = (nblk + 255) / 256;
+  const int64_t K = (nblk + NT - 1) / NT;
   const int64_t lo = (int64_t)tid * K, hi = min(lo + K, nblk);
-  int16_t *v = dcv + d.coef_off;
   int s0 = 0, s1 = 0, s2 = 0, flag = 0;
   int b0 = 0;
   int64_t sp0 = 0;
@@ -486,36 +481,45 @@ __global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ des
       sp = sp + 1 == seglen ? 0 : sp + 1;
     }
   }
-  // inclusive segmented scan of (flag, s0, s1, s2) over the threads
-  s_f[tid] = flag;
-  s_v[0][tid] = s0;
-  s_v[1][tid] = s1;
-  s_v[2][tid] = s2;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    int pf = 0, p0 = 0, p1 = 0, p2 = 0;
-    if (tid >= off) {
-      pf = s_f[tid - off];
-      p0 = s_v[0][tid - off];
-      p1 = s_v[1][tid - off];
-      p2 = s_v[2][tid - off];
-    }
-    __syncthreads();
-    if (tid >= off && !flag) {
+  // segmented scan of (flag, s0, s1, s2) over the threads: within each wave
+  // by lane shifts, then across the NT/64 wave totals (one barrier)
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int pf = __shfl_up(flag, off), p0 = __shfl_up(s0, off), p1 = __shfl_up(s1, off),
+              p2 = __shfl_up(s2, off);
+    if (lane >= off && !flag) {
       s0 += p0;
       s1 += p1;
       s2 += p2;
-      s_v[0][tid] = s0;
-      s_v[1][tid] = s1;
-      s_v[2][tid] = s2;
     }
-    flag |= pf;
-    s_f[tid] = flag;
-    __syncthreads();
+    flag |= lane >= off ? pf : 0;
   }
-  int r0 = tid > 0 ? s_v[0][tid - 1] : 0;
-  int r1 = tid > 0 ? s_v[1][tid - 1] : 0;
-  int r2 = tid > 0 ? s_v[2][tid - 1] : 0;
+  if (lane == 63) {
+    scr[4 * wave] = flag;
+    scr[4 * wave + 1] = s0;
+    scr[4 * wave + 2] = s1;
+    scr[4 * wave + 3] = s2;
+  }
+  __syncthreads();
+  // the carry into this wave: the segmented sum of the earlier waves' totals
+  int r0 = 0, r1 = 0, r2 = 0;
+  for (int w = 0; w < wave; ++w) {
+    const bool f = scr[4 * w] != 0;
+    r0 = (f ? 0 : r0) + scr[4 * w + 1];
+    r1 = (f ? 0 : r1) + scr[4 * w + 2];
+    r2 = (f ? 0 : r2) + scr[4 * w + 3];
+  }
+  {
+    // exclusive within the wave: the previous lane's inclusive value
+    const int pf = __shfl_up(flag, 1), p0 = __shfl_up(s0, 1), p1 = __shfl_up(s1, 1),
+              p2 = __shfl_up(s2, 1);
+    if (lane > 0) {
+      r0 = (pf ? 0 : r0) + p0;
+      r1 = (pf ? 0 : r1) + p1;
+      r2 = (pf ? 0 : r2) + p2;
+    }
+  }
   int b = b0;
   int64_t sp = sp0;
   for (int64_t x = lo; x < hi; ++x) {
@@ -531,8 +535,20 @@ __global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ des
   }
 }
 
+// k_dc_scan: the DC predictors of the serial decoder's images (the parallel
+// decoder's workgroups scan their own image after the write pass).
+__global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ descs,
+                                                 int16_t *__restrict__ dcv,
+                                                 const int32_t *__restrict__ status) {
+  __shared__ int32_t scr[4 * 256 / 64];
+  const int img = blockIdx.x;
+  // progressive: dcv holds the final DC; sub_bits > 0: k_huff_image
+  if (status[img] != 0 || descs[img].nseg == 0 || descs[img].sub_bits > 0) return;
+  dc_scan_image<256>(descs[img], dcv + descs[img].coef_off, (LDS_AS int32_t *)scr);
+}
+
 hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
-  if (p.n == 0) return hipSuccess;
+  if (p.n_serial == 0) return hipSuccess;
   hipLaunchKernelGGL(k_dc_scan, dim3(p.n), dim3(256), 0, s, p.descs, w.dcv, w.status);
   return hipGetLastError();
 }
@@ -662,6 +678,7 @@ struct ImgLds {
   int32_t need_lanes, need_waves, memo_hits; // diagnostic counters (summed over rounds)
 };
 static_assert(sizeof(ImgLds) + 512 <= kHuffStaticLds, "k_huff_image static LDS");
+static_assert(sizeof(ImgLds) >= 4 * (kHuffThreads / 64) * sizeof(int32_t), "dc_scan_image scratch");
 
 // Exclusive prefix of v over the 1024-lane workgroup; contains __syncthreads.
 __device__ __forceinline__ int block_excl_scan1024(int v, int32_t *scratch, int *total) {
@@ -910,6 +927,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   const uint64_t t_scan = wall_clock64();
 
   // ---- write pass from the true entry ----
+  bool trunc = false;
   if (live) {
     int cursor = pre - sh.ex_p[sh.seg_first[g.si]] - 1; // segment-relative block, -1 before the DC
     const int total = sg.mcu_count * d.bpm;
@@ -920,10 +938,16 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     R.seek(g.pbias + wp);
     write_run(R, st, dec, wstop, cursor, total, reinterpret_cast<uint4 *>(coef + d.coef_off * 64), blk0,
               coef_npad(d), dcv + d.coef_off + blk0);
-    if (g.j == sg.sub_count - 1 && cursor + 1 < total) status[img] = 3; // ran out of data
+    if (g.j == sg.sub_count - 1 && cursor + 1 < total) {
+      status[img] = 3; // ran out of data
+      trunc = true;
+    }
   }
+  // the image's DC differences are complete. The barrier's workgroup-scope
+  // fence publishes them to the other waves (one CU, one vector L1); an
+  // agent-scope fence would write back and invalidate the XCD's whole L2.
+  trunc = __syncthreads_or(trunc);
   // diagnostic phase times (10 ns ticks summed over images; ldt_debug_counters)
-  __syncthreads();
   if (dbg && tid == 0) {
     const uint64_t t_end = wall_clock64();
     atomicAdd(dbg + 9, (int)(t_ph1 - t_setup));
@@ -933,6 +957,11 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     atomicAdd(dbg + 13, sh.need_lanes);
     atomicAdd(dbg + 14, sh.need_waves);
     atomicAdd(dbg + 4, sh.memo_hits);
+  }
+  // ---- DC predictors (the serial path runs k_dc_scan instead) ----
+  if (!trunc) {
+    __syncthreads(); // sh is free from here: its first 256 bytes are the scan scratch
+    dc_scan_image<kHuffThreads>(d, dcv + d.coef_off, (LDS_AS int32_t *)&sh);
   }
 }
 

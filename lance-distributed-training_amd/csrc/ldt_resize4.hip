@@ -148,6 +148,7 @@ struct Geom4 {
   int spad;        // staging row stride in dwords (multiple of 4)
   int ntask;       // n * nbands
   int wave_bytes;  // LDS per wave
+  int fill;        // JPEG: this launch zero-fills failed images' bands (label -100)
 };
 
 constexpr int kKvRows = 16; // vertical coefficient rows cached per wave
@@ -184,7 +185,18 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   const int task = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kResizeWaves + wave);
   if (task >= g.ntask) return;
   const int img = task / g.nbands, band = task - img * g.nbands;
-  if (kJpeg && (status[img] != 0 || resize_fast420(descs[img]) != (SRC == 0))) return;
+  if (kJpeg && status[img] != 0) {
+    // a failed image's band: zeros (and label -100), by one of the launches
+    const int oy0 = band * g.bh, nb = min(g.bh, kOut - oy0);
+    if (!g.fill || nb <= 0) return;
+    if (band == 0 && lane == 0 && out_labels != nullptr) out_labels[img] = -100;
+    float4 *o = reinterpret_cast<float4 *>(out + (int64_t)img * 3 * kOut * kOut + oy0 * kOut);
+    const int per = nb * kOut / 4; // float4s of the band in one channel plane
+    for (int c = 0; c < 3; ++c)
+      for (int i = lane; i < per; i += 64) o[c * (kOut * kOut / 4) + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  if (kJpeg && resize_fast420(descs[img]) != (SRC == 0)) return;
   int W, H;
   if constexpr (kJpeg) {
     W = descs[img].width;
@@ -579,12 +591,15 @@ bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t
   if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g), g)) return false;
   RawSrc raw{nullptr, 0, 0, 0};
   // fast-path images and the rest go to separate kernels (each skips the
-  // other's images); a batch of one kind launches one kernel
+  // other's images); a batch of one kind launches one kernel. The first
+  // launch also writes the failed images (k_fill_failed's job otherwise).
+  g.fill = 1;
   if (p.n_fast420 > 0) {
     if (!dispatch4<0>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s,
                       err))
       return false;
     if (*err != hipSuccess || p.n_fast420 == p.n) return true;
+    g.fill = 0;
   }
   return dispatch4<2>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s,
                       err);
@@ -597,6 +612,7 @@ bool launch_resize4_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, i
   if (ks_h > 11) return false;
   if (!make_geom4(n, wd, h, ks_h, 1, g)) return false;
   if (!make_geom4(n, wd, h, ks_h, waves_target4(g), g)) return false;
+  g.fill = 0;
   RawSrc raw{hwc, cell_stride, h, wd};
   const bool al16 = (((uintptr_t)hwc) & 15) == 0 && (cell_stride & 15) == 0 && ((wd * 3) & 15) == 0 &&
                     wd <= 1024;

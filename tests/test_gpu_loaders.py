@@ -156,6 +156,24 @@ def test_failed_rows_are_defined_and_prefetch_raises_before_yield():
     assert np.array_equal(img[0].cpu().numpy(), oracle.jpeg_to_tensor(good)) and int(lbl[0]) == 7
     with pytest.raises(ldt_amd.ImageDecodeError):
         pipe.check()
+    # k_resize4 writes the failed rows: batches with one and with both of its
+    # launches (4:2:0 fast-path images next to 4:4:4 ones)
+    g444 = synth.encode(synth.field(96, 72, 8), subsampling="4:4:4")
+    for cells in ([g444, bad, g444], [good, bad, g444, bad]):
+        n = len(cells)
+        rb2 = pa.RecordBatch.from_arrays([pa.array(cells, pa.binary()), pa.array(list(range(n)), pa.int64())],
+                                         names=["image", "label"])
+        torch.full((n, 3, 224, 224), float("nan"), device="cuda")
+        img, lbl, ready = pipe.decode(rb2, wait=False)
+        ready()
+        torch.cuda.synchronize()
+        for k, c in enumerate(cells):
+            if c is bad:
+                assert torch.count_nonzero(img[k]).item() == 0 and int(lbl[k]) == -100
+            else:
+                assert np.array_equal(img[k].cpu().numpy(), oracle.jpeg_to_tensor(c)) and int(lbl[k]) == k
+        with pytest.raises(ldt_amd.ImageDecodeError):
+            pipe.check()
     fn = ldt_amd.make_to_tensor_fn(depth=3, prefetch=2)
     good_rb = pa.RecordBatch.from_arrays([pa.array([good], pa.binary()), pa.array([1], pa.int64())],
                                          names=["image", "label"])
