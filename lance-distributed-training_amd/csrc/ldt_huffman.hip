@@ -333,7 +333,7 @@ __device__ __forceinline__ void store_group(uint4 *__restrict__ p, uint64_t lo, 
 // Coefficient-writing decode of one range: from the reader's position until
 // it reaches `stop` or the segment's `total` blocks are complete. cursor is
 // the current block (segment-relative, -1 before the first DC). DC symbols
-// store their difference in dcv_seg[cursor] (k_dc_scan adds the predictors);
+// store their difference in dcv_seg[cursor] (dc_scan_image adds the predictors);
 // nonzero AC coefficients go to the image's group planes (block
 // seg_blk0 + cursor of coef_img, see coef_piece), which are all zero
 // beforehand (k_idct clears every block it reads). The loop body is straight-line: every
@@ -583,8 +583,8 @@ hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
 //            flows to the right);
 //   prefix   exclusive scan of the block counts: each range's first block;
 //   write    every lane decodes its range again from its true entry and stores
-//            coefficients (zigzag groups) and DC differences (k_dc_scan adds
-//            the predictors).
+//            coefficients (zigzag groups) and DC differences;
+//   dc       the workgroup adds the DC predictors (dc_scan_image).
 // An image with more than kMaxParSegs restart segments takes k_huff_serial
 // instead: one lane per segment is already parallel there.
 // ===========================================================================

@@ -508,7 +508,7 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
       ws[kZigzagNat[8 * r + 2 * j + 1]] = __mul24(hi, (int32_t)(qw[j] >> 16));
     }
   }
-  ws[0] = (int32_t)dcv[d.coef_off + blk] * (int32_t)q[0]; // DC: absolute value from k_dc_scan
+  ws[0] = (int32_t)dcv[d.coef_off + blk] * (int32_t)q[0]; // DC: absolute value after the predictor scan
   // pass 1: columns (CONST_BITS 13, PASS1_BITS 2). A column whose AC terms are
   // all zero gives DC << 2 exactly (jidctint.c shortcut); the butterfly runs
   // when any lane of the wave needs it.
@@ -557,7 +557,8 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
   }
 }
 
-// Rows whose decode failed: the resize kernels skip them, so their outputs
+// Rows whose decode failed, behind the streaming k_resize fallback (k_resize4
+// writes them itself): k_resize skips them, so their outputs
 // are set here to defined values — zeros for the image and -100 for the label
 // (torch.nn.CrossEntropyLoss's default ignore_index) — in case an
 // asynchronous consumer (prefetching iterators) uses the batch before the

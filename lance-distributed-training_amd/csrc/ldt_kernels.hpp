@@ -71,7 +71,7 @@ struct DevWork {
   int16_t *coef;        // AC coefficients (the DC slot of each block is unused), in
                         // group planes (coef_piece); all zero between batches (k_idct
                         // clears every block it reads)
-  int16_t *dcv;         // per block: DC difference (Huffman), then absolute DC (k_dc_scan)
+  int16_t *dcv;         // per block: DC difference (Huffman), then absolute DC (dc_scan_image)
   uint8_t *planes;      // component planes
   int32_t *status;      // per image
   int4 *ds_cnt;         // per destuff chunk: kept bytes, RSTn markers, end marker seen
