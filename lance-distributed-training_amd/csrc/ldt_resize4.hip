@@ -18,6 +18,7 @@
 // Pillow Resample.c ImagingResample (horizontal pass first, uint8 between).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ldt_device.hpp"
 #include "ldt_kernels.hpp"
@@ -579,7 +580,10 @@ static int waves_target4(const Geom4 &g) {
   int wg = (160 * 1024) / (3072 + kResizeWaves * g.wave_bytes);
   if (wg > 6) wg = 6;
   if (wg < 1) wg = 1;
-  return cus * kResizeWaves * wg;
+  // tuning knob: more, shorter bands fill the pipeline's CU
+  // gaps better but cost the kernel's own efficiency
+  static const int pct = getenv("LDT_RESIZE_WAVES_PCT") ? atoi(getenv("LDT_RESIZE_WAVES_PCT")) : 100;
+  return cus * kResizeWaves * wg * (pct > 0 ? pct : 100) / 100;
 }
 
 bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
