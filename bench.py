@@ -1,20 +1,29 @@
 """Benchmark of the MI355X batch-decode path (BASELINE.json metric).
 
-One "step" = one batch of synthetic JPEG cells (already resident in HBM)
-through the whole hot path: marker walk + plan upload, destuff, Huffman
-decode, IDCT, fused upsample/colour/Resize(224,224)/ToTensor store, labels.
+One "step" = one batch of synthetic JPEG cells through the whole hot path:
+marker walk + plan upload, destuff, Huffman decode, IDCT, fused
+upsample/colour/Resize(224,224)/ToTensor store, labels.
 Default workload (N=1 and per rank for N>1, weak scaling): BASELINE.json
 configs[1] — 512x512 baseline JPEG, 4:2:0, q90, batch 256 per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c4|c5|c2p]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3|c4|c5|c2p]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line. The CPU baseline (rank 0, N=1 only) times the
-reference's own CPU path on this host in this run: the map-style DataLoader
-harness with the PIL collate_fn (lance_map_style.py:21-44, :54-69) at
-num_workers 8 and at the box's CPU share, and the iterable to_tensor_fn in
-one process (cpu_baseline below). value_host_input is the PCIe-inclusive rate
-of the same steps (host RecordBatches).
+Three legs of the same workload, each timed between barriers (max over ranks):
+  value             cells resident in HBM when the timed region starts (the
+                    driver contract); everything else of the path is timed;
+  value_host_input  the plug-in boundary: host pa.RecordBatches through the
+                    pipelined to_tensor_fn (pinned copy + H2D every step);
+  value_dataset     the reference's iterable loop: an Arrow/Lance dataset of the
+                    workload's cells read through LanceDataset + the sampler
+                    (ShardedBatchSampler; ShardedFragmentSampler(pad=True) with
+                    its RCCL all_reduce(MAX) for c4 = configs[3]) + to_tensor_fn,
+                    one full epoch (plan included) per rank.
+Each is whole-job (all ranks) with a *_per_gpu twin. Rank 0 prints ONE JSON
+line. The CPU baseline (rank 0, N=1 only) times the reference's own CPU path
+on this host in this run: the map-style DataLoader harness with the PIL
+collate_fn (lance_map_style.py:21-44, :54-69) at num_workers 8 and at the
+box's CPU share, and the iterable to_tensor_fn in one process.
 """
 from __future__ import annotations
 
@@ -34,14 +43,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 OUT_BYTES = 3 * 224 * 224 * 4  # 602,112 B per image (float32 CHW)
 
 WORKLOADS = {
-    "c2": dict(desc="512x512 baseline JPEG 4:2:0 q90 (BASELINE configs[1]), to_tensor_fn", batch=256),
-    "c1": dict(desc="FOOD101-shaped 512x384/384x512/512x512 JPEG, PIL defaults q75 4:2:0 (configs[0]/[2] data)",
-               batch=128),
-    "c4": dict(desc="ImageNet-shaped ~500x375 variable JPEG q90 with restart markers (configs[3] data)", batch=128),
+    "c2": dict(desc="512x512 baseline JPEG 4:2:0 q90 (BASELINE configs[1]), to_tensor_fn", batch=256,
+               sampler="batch"),
+    "c1": dict(desc="FOOD101-shaped 512x384/384x512/512x512 JPEG, PIL defaults q75 4:2:0 (configs[0] data)",
+               batch=128, sampler="batch"),
+    "c3": dict(desc="FOOD101 LanceDataset iterable + ShardedBatchSampler, batch 128/rank (BASELINE configs[2]); "
+                    "FOOD101-shaped PIL-default q75 cells", batch=128, sampler="batch"),
+    "c4": dict(desc="ImageNet-shaped ~500x375 variable JPEG q90 with restart markers, ShardedFragmentSampler "
+                    "pad=True over uneven fragments (BASELINE configs[3])", batch=128, sampler="fragment"),
     "c5": dict(desc="raw uint8 HWC 1024x1024 -> Resize 224 + Normalize (configs[4])", batch=1024),
     # not a BASELINE config: the c2 images encoded progressive (SOF2), to
     # measure the serial per-scan path
-    "c2p": dict(desc="c2's 512x512 q90 4:2:0 images as progressive JPEG (SOF2)", batch=256),
+    "c2p": dict(desc="c2's 512x512 q90 4:2:0 images as progressive JPEG (SOF2)", batch=256, sampler="batch"),
 }
 
 
@@ -52,14 +65,16 @@ def make_cells(workload: str, n: int, seed: int):
         return synth.q90_512(n, seed=seed)
     if workload == "c2p":
         return synth.q90_512(n, seed=seed, progressive=True)
-    if workload == "c1":
+    if workload in ("c1", "c3"):
         return synth.food101_like(n, seed=seed)
     if workload == "c4":
         return synth.imagenet_like(n, seed=seed)
     raise ValueError(workload)
 
 
-CPU_SHARE = 16  # CPUs of the GPU box a run may use per GPU (os.cpu_count() shows the whole host)
+# CPUs of the GPU box a one-GPU run may use (os.sched_getaffinity shows the
+# whole host there); LDT_CPU_SHARE overrides it on hosts with another share
+CPU_SHARE = int(os.environ.get("LDT_CPU_SHARE", "16"))
 
 
 def _rates(times, imgs):
@@ -67,7 +82,7 @@ def _rates(times, imgs):
     return {"best": round(r[-1], 1), "median": round(r[len(r) // 2], 1), "reps": [round(x, 1) for x in r]}
 
 
-def cpu_baseline(cells, labels, batch: int = 128, reps: int = 5):
+def cpu_baseline(cells, labels, batch: int = 128, reps: int = 7, workers=None):
     """The reference's CPU path on this host, in this run.
 
     map-style legs: lance_map_style.py:54-69's harness, i.e. a stock torch
@@ -75,8 +90,8 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 5):
     (oracle.pil_collate_fn = lance_map_style.py:21-44: Pillow
     open/convert/Resize((224,224))/to_tensor, stack), batch 128 (config 1),
     pin_memory=True, persistent spawn workers; num_workers = 8 (the reference
-    default, :137) and the box's CPU share. Each leg: one batch per worker
-    (plus the prefetch queue) to warm up, then `reps` timed runs of
+    default, :137) and the box's CPU share (or `workers`). Each leg: one batch
+    per worker (plus the prefetch queue) to warm up, then `reps` timed runs of
     2 x num_workers batches; best and median img/s.
     iterable leg: lance_iterable.py:38-50's decode_tensor_image on
     RecordBatches in the main process (num_workers=0, :75-77)."""
@@ -94,14 +109,16 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 5):
     import ldt_amd as lds
 
     tmp = tempfile.mkdtemp(prefix="ldt_cpu_")
+    host = len(os.sched_getaffinity(0))
+    if workers is None:
+        workers = sorted({8, min(host, CPU_SHARE)})
     try:
         n = len(cells)
         lds.write_dataset(pa.table({"image": pa.array(cells, pa.binary()),
                                     "label": pa.array(np.asarray(labels, np.int64))}), tmp)
         ds = lds.SafeLanceDataset(tmp)
-        host = len(os.sched_getaffinity(0))
         legs = []
-        for w in sorted({8, min(host, CPU_SHARE)}):
+        for w in workers:
             need = batch * w * (4 + 2 * reps)  # warm-up + timed
             order = [i % n for i in range(need)]
             loader = lds.get_safe_loader(ds, batch_size=batch, sampler=order, num_workers=w,
@@ -140,9 +157,11 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 5):
                    f"PIL collate_fn, batch {batch}, pin_memory, persistent spawn workers), "
                    f"{reps} x 2*num_workers timed batches per leg after warm-up; Pillow {pil_version} / "
                    f"libjpeg-turbo {features.version_feature('libjpeg_turbo')}; host affinity {host} CPUs "
-                   f"(a one-GPU run may use {CPU_SHARE}); value = median of the "
-                   f"num_workers={ref['num_workers']} leg (lance_map_style.py:137 default)"),
+                   f"(a one-GPU run may use {CPU_SHARE}; the whole-host leg is --cpu-workers {host}); "
+                   f"value = median of the num_workers={ref['num_workers']} leg (lance_map_style.py:137 default)"),
         "legs": legs,
+        "host_cpus": host,
+        "cpu_share": CPU_SHARE,
         "torch_threads": torch.get_num_threads(),
     }
 
@@ -155,13 +174,18 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--input", choices=("resident", "host"), default="resident",
-                    help="resident: cells already in HBM (value); host: Arrow RecordBatches in host "
-                         "memory through the pipelined to_tensor_fn (PCIe-inclusive, DESIGN.md §7)")
+    ap.add_argument("--cpu-workers", default="",
+                    help="comma-separated num_workers legs of the CPU baseline (default: 8 and the CPU share)")
     ap.add_argument("--no-stage-events", action="store_true",
                     help="time without the per-stage HIP events (no roofline)")
     ap.add_argument("--depth", type=int, default=3,
                     help="batches in flight (ldt_amd.DecodePipeline: one context + HIP stream each)")
+    ap.add_argument("--dataset-batches", type=int, default=12,
+                    help="batches per rank of one epoch of the dataset leg (0: skip the leg)")
+    ap.add_argument("--dataset-epochs", type=int, default=2,
+                    help="epochs in the dataset leg's timed region (each re-plans, as a training loop does)")
+    ap.add_argument("--registered", action="store_true",
+                    help="also time the host leg with the cell buffers page-locked in place (ldt_register_host)")
     args = ap.parse_args()
 
     import numpy as np
@@ -193,6 +217,27 @@ def main():
     ctx.set_option(_lib.OPT_SYNC_STATUS, 0)
     ctx.set_option(_lib.OPT_PROFILE, 0 if args.no_stage_events else 1)
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x: float) -> float:
+        t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(step, steps, warmup):
+        for _ in range(warmup):
+            step()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0)
+
     cells = None
     if args.workload == "c5":
         # synthetic uniform uint8 HWC 1024x1024 generated directly in HBM
@@ -216,91 +261,73 @@ def main():
             host_batches.append(pa.RecordBatch.from_arrays(
                 [pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
                 names=["image", "label"]))
-            if args.input == "host":
-                batches.append(host_batches[-1])
-            else:
-                batches.append(ldt_amd.ResidentBatch(cells, labels, device=dev))
+            batches.append(ldt_amd.ResidentBatch(cells, labels, device=dev))
         px = [ldt_amd_dims(c) for c in cells_all[:B]]
         bytes_per_img = float(np.mean([h * w * 3 for (h, w) in px])) + OUT_BYTES
         comp_bytes = float(np.mean([len(c) for c in cells_all]))
         it = [0]
         pipe = ldt_amd.DecodePipeline(depth=args.depth, device=dev, profile=not args.no_stage_events)
-        for c in pipe.ctxs:  # tuning knobs (default minimum S = 256 bits, fitted per image)
-            if os.environ.get("LDT_SUBSEQ_BITS"):
-                c.set_option(_lib.OPT_SUBSEQ_BITS, int(os.environ["LDT_SUBSEQ_BITS"]))
-            if os.environ.get("LDT_SYNC_WARM"):
-                c.set_option(_lib.OPT_SYNC_WARM, int(os.environ["LDT_SYNC_WARM"]))
 
         def step():
             b = batches[it[0] % nb]
             it[0] += 1
             return pipe.decode(b)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
+    # every slot context sees >= 2 calls (both pinned slots allocated) before timing
+    warm = max(args.warmup, 2 * args.depth + 1) if args.workload != "c5" else args.warmup
     prof = ctx if args.workload == "c5" else pipe
+    for _ in range(warm):
+        step()
     barrier()
     prof.stage_times(reset=True)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed_max = timed(step, args.steps, 0)
     stages = prof.stage_times(reset=True)
     if args.workload != "c5":
         pipe.check()  # every decoded image status OK
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
-    total_imgs = B * args.steps * world
-    value = total_imgs / elapsed_max
+    value = B * args.steps * world / elapsed_max
 
-    # PCIe-inclusive rate in the same run: the same steps with
-    # the cells in host Arrow RecordBatches through the pipelined to_tensor_fn
-    def host_rate(bs):
-        hp = ldt_amd.DecodePipeline(depth=args.depth, device=dev)
-        for k in range(max(args.warmup, 2)):
-            hp.decode(bs[k % nb])
-        barrier()
-        th0 = time.perf_counter()
-        for k in range(args.steps):
-            hp.decode(bs[k % nb])
-        barrier()
-        th = torch.tensor([time.perf_counter() - th0], dtype=torch.float64,
-                          device=dev if backend == "nccl" else "cpu")
-        if world > 1:
-            dist.all_reduce(th, op=dist.ReduceOp.MAX)
-        hp.check()
-        return B * args.steps * world / float(th.item())
+    # the plug-in boundary: the same steps with the cells in
+    # host Arrow RecordBatches through the pipelined to_tensor_fn
+    def host_rate(bs, register=False):
+        fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev, register=register)
+        fn.pipeline.set_option(_lib.OPT_HOST_TIMING, 1)
+        k = [0]
 
-    value_host = value_registered = None
-    if args.workload != "c5" and args.input == "resident":
-        value_host = host_rate(host_batches)
-        # the same host batches with their image buffers page-locked in place
-        # (ldt_register_host): DMA from the caller's pages, no staging memcpy
-        # (optional leg: a box whose memlock limit refuses the pinning reports null)
-        try:
-            for b in host_batches:
-                ldt_amd.register_host(b.column(0), device=dev)
-            value_registered = host_rate(host_batches)
-        except ldt_amd.LdtError as e:
-            print(f"bench: registered host leg skipped: {e}", file=sys.stderr)
-        finally:
-            for b in host_batches:
-                ldt_amd.unregister_host(b.column(0))
+        def hstep():
+            fn(bs[k[0] % len(bs)])
+            k[0] += 1
+
+        for _ in range(warm):
+            hstep()
+        barrier()
+        fn.pipeline.host_times(reset=True)
+        t = timed(hstep, args.steps, 0)
+        fn.check()
+        us, calls = fn.pipeline.host_times(reset=True)
+        if register:
+            fn.release()
+        return B * args.steps * world / t, {k_: round(v / max(calls, 1), 1) for k_, v in us.items()}
+
+    value_host = value_registered = host_us = None
+    if args.workload != "c5":
+        value_host, host_us = host_rate(host_batches)
+        if args.registered:
+            try:
+                value_registered, _ = host_rate(host_batches, register=True)
+            except ldt_amd.LdtError as e:
+                print(f"bench: registered host leg skipped: {e}", file=sys.stderr)
+
+    value_dataset = None
+    dataset_info = None
+    if args.workload != "c5" and args.dataset_batches > 0:
+        value_dataset, dataset_info = dataset_rate(args, wl, B, world, rank, dev, cells_all, labels_all,
+                                                   barrier, max_over_ranks)
 
     # standalone launch durations (one batch in flight, after the timed region)
     standalone = None
     if args.workload != "c5" and not args.no_stage_events:
         solo = ldt_amd.DecodePipeline(depth=1, device=dev, profile=True)
-        for k in range(2):
+        for k in range(3):
             solo.decode(batches[k % nb])
         barrier()
         solo.stage_times(reset=True)
@@ -330,13 +357,15 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": (f"synthetic (seeded PIL-encoded JPEG cells {'resident in HBM' if args.input == 'resident' else 'in host Arrow RecordBatches, copied over PCIe every step'}; FOOD101 offline-unavailable)"
+        "data": ("synthetic (seeded PIL-encoded JPEG cells; value: resident in HBM when the timed region starts; "
+                 "value_host_input: host Arrow RecordBatches through to_tensor_fn; FOOD101 offline-unavailable)"
                  if args.workload != "c5" else "synthetic (uniform uint8 HWC generated in HBM)"),
         "config": {"workload": f"{args.workload}: {wl['desc']}", "per_gpu_batch": B, "global_batch": B * world,
                    "parallelism": f"dp{world} (independent shards, no data-path collective)",
                    "pipeline_depth": 1 if args.workload == "c5" else args.depth,
-                   "input": "resident" if args.workload == "c5" else args.input,
+                   "input": "resident",
                    "output": "float32[N,3,224,224] + int64[N] on device"},
+        "value_per_gpu": round(value / world, 1),
         "roofline": {
             "kernel": "k_resize (fused chroma upsample + YCbCr->RGB + BILINEAR 224 + ToTensor store)"
                       if args.workload != "c5" else "k_resize<raw> (BILINEAR 224 + Normalize store)",
@@ -352,6 +381,19 @@ def main():
         "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items()},
         "dominant_stage": dominant,
     }
+    if value_host is not None:
+        res["value_host_input"] = round(value_host, 1)
+        res["value_host_input_per_gpu"] = round(value_host / world, 1)
+        res["value_host_input_note"] = ("the same steps with the cells in host pa.RecordBatches through the "
+                                        "pipelined to_tensor_fn (make_to_tensor_fn(depth)): pinned copy "
+                                        "overlapped with the header walk + H2D every step")
+        res["host_us_per_call"] = host_us
+    if value_registered is not None:
+        res["value_host_registered"] = round(value_registered, 1)
+    if value_dataset is not None:
+        res["value_dataset"] = round(value_dataset, 1)
+        res["value_dataset_per_gpu"] = round(value_dataset / world, 1)
+        res["dataset_leg"] = dataset_info
     if standalone is not None:
         sa_ms, sa_n = standalone["resize"]
         sa_s = sa_ms / max(sa_n, 1) / 1e3
@@ -377,16 +419,14 @@ def main():
         res["decode_efficiency"] = dec
     if args.workload != "c5":
         res["config"]["compressed_bytes_per_img"] = round(comp_bytes, 1)
-    if value_host is not None:
-        res["value_host_input"] = round(value_host, 1)
-        res["value_host_input_note"] = ("same steps with the cells in host pa.RecordBatches (pinned copy + "
-                                        "H2D every step, to_tensor_fn boundary); value keeps them in HBM")
-    if value_registered is not None:
-        res["value_host_registered"] = round(value_registered, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "c5":
-        res["cpu_baseline"] = cpu_baseline(cells_all, labels_all)
+        workers = [int(x) for x in args.cpu_workers.split(",") if x] or None
+        res["cpu_baseline"] = cpu_baseline(cells_all, labels_all, workers=workers)
         res["gpu_over_cpu"] = {f"num_workers={leg['num_workers']}": round(value / leg["median"], 1)
                                for leg in res["cpu_baseline"]["legs"]}
+        if value_host is not None:
+            res["gpu_over_cpu_host_input"] = {f"num_workers={leg['num_workers']}": round(value_host / leg["median"], 1)
+                                              for leg in res["cpu_baseline"]["legs"]}
     elif rank == 0 and world == 1 and args.workload == "c5" and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_raw(raw[:8].cpu().numpy())
         res["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 2)
@@ -394,6 +434,90 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over_ranks):
+    """The reference's iterable loop (lance_iterable.py:53-72, :86-116) over an
+    Arrow/Lance dataset of this workload's cells: LanceDataset + the sampler +
+    the pipelined to_tensor_fn, `dataset_epochs` full epochs per rank in the
+    timed region (each epoch's plan — device shard kernel, and for pad=True
+    the all_reduce(MAX) over the process group — included). Rank 0 writes the
+    dataset (the workload's cells repeated to `dataset_batches` batches per
+    rank) into fragments of the config's shape; every rank then runs one
+    untimed epoch and the timed ones. Padding batches (pad=True) are decoded
+    and counted. Returns (whole-job img/s, info)."""
+    import shutil
+
+    import numpy as np
+    import pyarrow as pa
+
+    import ldt_amd
+
+    nbatch = args.dataset_batches
+    # FOOD101's fragments [12500 x 6, 750] (create_datasets/classification.py:16,60)
+    # scaled so that a rank reads about `nbatch` batches
+    if wl["sampler"] == "fragment":
+        # ShardedFragmentSampler: rank r owns fragments r, r+W, ...; at W = 8
+        # ranks 0-5 own a full fragment, rank 6 the short one, rank 7 none
+        F = max(1, round(nbatch / -(-6 // world))) * B
+    else:
+        # ShardedBatchSampler: global row ranges, nbatch per rank
+        F = -(-(nbatch * B * world * 12500 // 75750) // B) * B
+    sizes = [F] * 6 + [max(1, F * 750 // 12500)]
+    if wl["sampler"] != "fragment":
+        sizes = [F] * (nbatch * B * world // F) + ([nbatch * B * world % F] if nbatch * B * world % F else [])
+    rows = sum(sizes)
+    import tempfile
+
+    path = os.path.join(tempfile.gettempdir(), f"ldt_bench_ds_{os.environ.get('MASTER_PORT', '0')}_{args.workload}_{world}")
+    if rank == 0:
+        n = len(cells)
+        idx = np.arange(rows) % n
+        tbl = pa.table({"image": pa.array([cells[i] for i in idx], pa.binary()),
+                        "label": pa.array(np.asarray(labels, np.int64)[idx])})
+        ldt_amd.write_dataset(tbl, path, max_rows_per_file=F)
+        del tbl
+    barrier()
+    if wl["sampler"] == "fragment":
+        sampler = ldt_amd.ShardedFragmentSampler(rank=rank, world_size=world, pad=True)
+    else:
+        sampler = ldt_amd.ShardedBatchSampler(rank=rank, world_size=world)
+    fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev)
+    ds = ldt_amd.LanceDataset(path, batch_size=B, sampler=sampler, to_tensor_fn=fn)
+
+    def epoch():
+        imgs = 0
+        for b in ds:  # lance_iterable.py:107-109: batch["image"].to(device) is a no-op here
+            imgs += b["image"].shape[0]
+        return imgs
+
+    epoch()
+    fn.check()
+    barrier()
+    t0 = time.perf_counter()
+    imgs = sum(epoch() for _ in range(args.dataset_epochs))
+    barrier()
+    t = max_over_ranks(time.perf_counter() - t0)
+    fn.check()
+    tot_imgs = imgs
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        tt = torch.tensor([imgs], dtype=torch.int64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(tt)
+        tot_imgs = int(tt.item())
+    barrier()
+    if rank == 0:
+        shutil.rmtree(path, ignore_errors=True)
+    info = {"sampler": type(sampler).__name__ + ("(pad=True)" if wl["sampler"] == "fragment" else ""),
+            "rows": rows, "fragments": sizes if len(sizes) <= 16 else f"{len(sizes)} fragments",
+            "target_batches_per_rank": nbatch, "epochs": args.dataset_epochs,
+            "images_all_ranks": tot_imgs, "elapsed_ms_max": round(t * 1e3, 3),
+            "timing": "full epochs per rank (plan + every batch, padding included) between barriers, "
+                      "max over ranks",
+            "harness": "LanceDataset(path, batch_size, sampler, to_tensor_fn=make_to_tensor_fn(depth))"}
+    return tot_imgs / t, info
 
 
 PROFILE_ROUND = "r2"

@@ -66,11 +66,23 @@ extern "C" {
                                  S >= this that fits its slots in 1024 lanes   */
 #define LDT_OPT_PROFILE 4     /* 1: record HIP events around every stage on the
                                  caller's stream (read with ldt_stage_times)    */
-#define LDT_OPT_RESIZE_IMPL 5 /* 0 auto (default): one wave per band; 2: the
-                                 streaming workgroup kernel that serves sources
-                                 wider than 1120 px (cross-check)               */
+#define LDT_OPT_RESIZE_IMPL 5 /* 0 auto (default): 4:2:0 sources <= 512 px wide
+                                 two waves per band (k_resize420), the others one
+                                 wave per band (k_resize4); 1: k_resize4 for
+                                 all; 2: the streaming workgroup kernel that
+                                 serves sources wider than 1120 px (cross-check) */
 #define LDT_OPT_SYNC_WARM 7   /* parallel decoder phase 1 starts this % of S
                                  before each range (0..200, default 0)         */
+#define LDT_OPT_COPY_THREADS 8 /* threads of the context's host copy pool that
+                                 move a batch's cells into the pinned slot while
+                                 the calling thread walks the headers (0..31;
+                                 -1 = default, min(4, cores - 1))             */
+#define LDT_OPT_HOST_TIMING 9 /* 1: accumulate host phase times of every
+                                 decode call (read with ldt_host_times)        */
+#define LDT_OPT_RESIZE_WAVES_PCT 10 /* resize bands per batch as % of one full
+                                 wave of resize waves on the device (10..1000,
+                                 default 100); more bands fill the pipeline's
+                                 CU gaps, fewer keep the kernel efficient      */
 
 /* ---- stages reported by ldt_stage_times ---- */
 #define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */
@@ -154,6 +166,13 @@ int ldt_fetch_status(ldt_ctx *ctx, void *stream, int32_t *per_image_status, int6
  * ms_out[stage] and the number of timed launches into count_out[stage]
  * (arrays of LDT_NUM_STAGES). reset != 0 clears the accumulators after reading. */
 int ldt_stage_times(ldt_ctx *ctx, double *ms_out, int64_t *count_out, int reset);
+
+/* Host phase times (LDT_OPT_HOST_TIMING = 1), microseconds summed over the
+ * timed calls since the last reset, into us_out[LDT_NUM_HOST_PHASES]:
+ * pinned slot + copy start, header walk (overlaps the cell copy), plan blob,
+ * cell copy join + H2D enqueue, kernel launches, status; *calls_out = calls. */
+#define LDT_NUM_HOST_PHASES 6
+int ldt_host_times(ldt_ctx *ctx, double *us_out, int64_t *calls_out, int reset);
 
 /* Config 5: raw uint8 HWC cells (no JPEG) -> Resize(224,224) [+Normalize] ->
  * float32 [n,3,224,224]. `hwc` is a device pointer when hwc_is_device != 0,

@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <memory>
 #include <chrono>
@@ -54,11 +55,16 @@ struct PinBuf {
 
 // Host copies into the pinned ring (Arrow cells -> pinned -> HBM) are the
 // host-side bottleneck of the PCIe path: one core moves ~6-10 GB/s. A small
-// persistent pool per context splits a large copy into chunks.
+// persistent pool per context copies a batch's cells in chunks while the
+// calling thread walks the JPEG headers (decode_core): start() hands the copy
+// to the pool and returns, finish() joins in on the chunks still untaken and
+// waits for the rest. Chunks are claimed with one 64-bit ticket (generation in
+// the high half), so a thread still looping over an old copy can never take a
+// chunk of the next one.
 class CopyPool {
 public:
   explicit CopyPool(int nthreads) {
-    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this, i] { run(i + 1); });
+    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this] { run(); });
   }
   ~CopyPool() {
     {
@@ -69,58 +75,95 @@ public:
     cv_.notify_all();
     for (auto &t : th_) t.join();
   }
-  void copy(void *dst, const void *src, size_t n) {
-    const int parts = (int)th_.size() + 1;
-    if (n < ((size_t)1 << 20) || th_.empty()) {
+  int threads() const { return (int)th_.size(); }
+  void start(void *dst, const void *src, size_t n) {
+    if (th_.empty() || n < ((size_t)1 << 20)) {
       memcpy(dst, src, n);
+      sync_done_ = true;
       return;
     }
+    sync_done_ = false;
     {
       std::lock_guard<std::mutex> g(m_);
       dst_ = static_cast<uint8_t *>(dst);
       src_ = static_cast<const uint8_t *>(src);
       n_ = n;
-      parts_ = parts;
-      pending_ = parts - 1;
+      // ~4 chunks per thread (the caller joins late), at least 256 KB
+      const size_t parts = 4 * (th_.size() + 1);
+      chunk_ = std::max<size_t>(((n + parts - 1) / parts + 4095) & ~(size_t)4095, (size_t)1 << 18);
+      nchunks_ = (uint32_t)((n + chunk_ - 1) / chunk_);
+      done_ = 0;
       ++gen_;
+      ticket_.store((uint64_t)(uint32_t)gen_ << 32, std::memory_order_release);
     }
     cv_.notify_all();
-    part(0);
+  }
+  // Take part in the copy until no chunk is left, then wait for all of them.
+  void finish() {
+    if (sync_done_) return;
+    uint32_t g;
+    {
+      std::lock_guard<std::mutex> l(m_);
+      g = (uint32_t)gen_;
+    }
+    work(g);
     std::unique_lock<std::mutex> lk(m_);
-    done_cv_.wait(lk, [this] { return pending_ == 0; });
+    done_cv_.wait(lk, [this] { return done_ == nchunks_; });
+    sync_done_ = true;
   }
 
 private:
-  void part(int k) {
-    const size_t chunk = ((n_ + parts_ - 1) / parts_ + 63) & ~(size_t)63;
-    const size_t lo = std::min(n_, chunk * (size_t)k), hi = std::min(n_, lo + chunk);
-    if (hi > lo) memcpy(dst_ + lo, src_ + lo, hi - lo);
+  void work(uint32_t g) {
+    for (;;) {
+      // claim chunk i of generation g only (a fetch_add could consume a
+      // chunk of a newer copy that this thread then would not do)
+      uint64_t t = ticket_.load(std::memory_order_acquire);
+      do {
+        if ((uint32_t)(t >> 32) != g || (uint32_t)t >= nchunks_) return;
+      } while (!ticket_.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel,
+                                              std::memory_order_acquire));
+      const uint32_t i = (uint32_t)t;
+      const size_t lo = (size_t)i * chunk_, hi = std::min(n_, lo + chunk_);
+      memcpy(dst_ + lo, src_ + lo, hi - lo);
+      std::lock_guard<std::mutex> l(m_);
+      if (++done_ == nchunks_) done_cv_.notify_all();
+    }
   }
-  void run(int k) {
+  void run() {
     uint64_t seen = 0;
     for (;;) {
+      uint32_t g;
       {
         std::unique_lock<std::mutex> lk(m_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
         if (stop_) return;
+        g = (uint32_t)gen_;
       }
-      part(k);
-      {
-        std::lock_guard<std::mutex> g(m_);
-        if (--pending_ == 0) done_cv_.notify_one();
-      }
+      work(g);
     }
   }
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
   uint64_t gen_ = 0;
-  bool stop_ = false;
+  std::atomic<uint64_t> ticket_{0};
+  bool stop_ = false, sync_done_ = true;
   uint8_t *dst_ = nullptr;
   const uint8_t *src_ = nullptr;
-  size_t n_ = 0;
-  int parts_ = 1, pending_ = 0;
+  size_t n_ = 0, chunk_ = 0;
+  uint32_t nchunks_ = 0, done_ = 0;
+};
+
+// Host phases of decode_core (LDT_OPT_HOST_TIMING; read with ldt_host_times).
+enum HostPhase {
+  kHpSlot = 0, // waiting for the pinned slot, starting the cell copy
+  kHpParse,    // header walk + per-image plans (overlaps the cell copy)
+  kHpPlan,     // plan blob, device workspace sizing
+  kHpCopy,     // waiting for the cell copy to finish, H2D enqueue
+  kHpLaunch,   // kernel launches
+  kHpStatus,   // status copy, return
+  kHpCount
 };
 
 struct ldt_ctx {
@@ -131,6 +174,9 @@ struct ldt_ctx {
   int resize_impl = 0;
   int warm_pct = 0;
   int subseq_bits = 256; // minimum S of the parallel decoder
+  int resize_waves_pct = 100;
+  int copy_threads = -1; // -1: default (min(4, cores - 1))
+  bool host_timing = false;
   DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_dscnt;
   DevBuf d_perm; // DistributedSampler scratch: 3 int32 arrays of dataset_len
   std::unique_ptr<CopyPool> copier; // host -> pinned copies (created on first use)
@@ -145,6 +191,10 @@ struct ldt_ctx {
   hipEvent_t done_ev = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_last = false;
+  // the coefficient buffer must be all zero between batches (k_idct restores
+  // it); set while Huffman output may be in it without a k_idct launched
+  // after it, so the next call clears it
+  bool coef_dirty = false;
   std::unordered_map<std::string, int> hmap;
   std::vector<HuffTab> htabs;
   // stage profiling: one event per stage boundary, sets recycled once read
@@ -158,37 +208,27 @@ struct ldt_ctx {
   int64_t stage_cnt[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
   EvSet *cur_ev = nullptr;
   int64_t last_off_redo = -1; // debug counters of the last batch (plan blob offset)
-  double host_us[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}; // LDT_HOST_TIMING accumulators
+  double host_us[kHpCount] = {0, 0, 0, 0, 0, 0};
   int64_t host_calls = 0;
 };
 
 namespace {
 
-// Host-side phase times of decode_core (LDT_HOST_TIMING=1: averages printed
-// to stderr every 200 calls). Diagnostic only.
+// Host phase times of decode_core (LDT_OPT_HOST_TIMING = 1), accumulated per
+// context and read with ldt_host_times. Diagnostic only.
 struct HostTimer {
   ldt_ctx *c;
   bool on;
   std::chrono::steady_clock::time_point t;
-  explicit HostTimer(ldt_ctx *cc) : c(cc), on(host_timing_enabled()) {
+  explicit HostTimer(ldt_ctx *cc) : c(cc), on(cc->host_timing) {
     if (on) t = std::chrono::steady_clock::now();
-  }
-  static bool host_timing_enabled() {
-    static const bool e = getenv("LDT_HOST_TIMING") != nullptr;
-    return e;
   }
   void mark(int k) {
     if (!on) return;
     const auto n = std::chrono::steady_clock::now();
     c->host_us[k] += std::chrono::duration<double, std::micro>(n - t).count();
     t = n;
-    if (k == 5 && ++c->host_calls % 30 == 0) {
-      fprintf(stderr,
-              "ldt host us/call: parse %.1f slot-wait %.1f plan %.1f copies %.1f (cells %.1f memcpy+record %.1f prof_begin %.1f) launches %.1f status %.1f\n",
-              c->host_us[0] / 30, c->host_us[1] / 30, c->host_us[2] / 30, c->host_us[3] / 30,
-              c->host_us[6] / 30, c->host_us[7] / 30, c->host_us[8] / 30, c->host_us[4] / 30, c->host_us[5] / 30);
-      for (double &x : c->host_us) x = 0;
-    }
+    if (k == kHpStatus) ++c->host_calls;
   }
 };
 
@@ -241,30 +281,78 @@ int ensure_dev(ldt_ctx *c, DevBuf &b, size_t need, hipStream_t s, bool zero = fa
   return LDT_OK;
 }
 
-// Host ranges page-locked in place (ldt_register_host), for all contexts.
+// Host ranges page-locked in place (ldt_register_host), for all contexts. A
+// decode that DMAs from a range holds it (inflight) until its copy is
+// enqueued and marks the device it used; ldt_unregister_host drops the range,
+// waits for the holders, then synchronises every device that used it before
+// unpinning.
 struct HostRange {
   uintptr_t lo, hi;
+  int inflight = 0;
+  uint64_t devmask = 0;
 };
 std::mutex g_host_m;
-std::vector<HostRange> g_host_ranges;
+std::condition_variable g_host_cv;
+std::vector<std::shared_ptr<HostRange>> g_host_ranges;
+
+std::shared_ptr<HostRange> host_acquire(const void *p, size_t n, int dev) {
+  const uintptr_t lo = (uintptr_t)p, hi = lo + n;
+  std::lock_guard<std::mutex> l(g_host_m);
+  for (auto &r : g_host_ranges)
+    if (lo >= r->lo && hi <= r->hi) {
+      ++r->inflight;
+      r->devmask |= 1ull << (dev & 63);
+      return r;
+    }
+  return nullptr;
+}
+
+void host_release(std::shared_ptr<HostRange> &r) {
+  if (!r) return;
+  {
+    std::lock_guard<std::mutex> l(g_host_m);
+    --r->inflight;
+  }
+  g_host_cv.notify_all();
+  r.reset();
+}
 
 bool host_registered(const void *p, size_t n) {
   const uintptr_t lo = (uintptr_t)p, hi = lo + n;
   std::lock_guard<std::mutex> l(g_host_m);
-  for (const HostRange &r : g_host_ranges)
-    if (lo >= r.lo && hi <= r.hi) return true;
+  for (const auto &r : g_host_ranges)
+    if (lo >= r->lo && hi <= r->hi) return true;
   return false;
 }
 
-void pinned_copy(ldt_ctx *c, void *dst, const void *src, size_t n) {
+CopyPool &copier(ldt_ctx *c) {
   if (!c->copier) {
-    unsigned hw = std::thread::hardware_concurrency();
-    const char *e = getenv("LDT_COPY_THREADS");
-    int nt = e ? atoi(e) : (int)std::min(3u, hw > 1 ? hw - 1 : 0u);
-    c->copier.reset(new CopyPool(std::max(0, std::min(nt, 15))));
+    int nt = c->copy_threads;
+    if (nt < 0) {
+      const unsigned hw = std::thread::hardware_concurrency();
+      nt = (int)std::min(4u, hw > 1 ? hw - 1 : 0u);
+    }
+    c->copier.reset(new CopyPool(std::max(0, std::min(nt, 31))));
   }
-  c->copier->copy(dst, src, n);
+  return *c->copier;
 }
+
+void pinned_copy(ldt_ctx *c, void *dst, const void *src, size_t n) {
+  CopyPool &p = copier(c);
+  p.start(dst, src, n);
+  p.finish();
+}
+
+// Joins an asynchronous cell copy on every exit path of decode_core: the
+// caller's host buffer is borrowed only for the duration of the call.
+struct CopyJoin {
+  CopyPool *p = nullptr;
+  void wait() {
+    if (p) p->finish();
+    p = nullptr;
+  }
+  ~CopyJoin() { wait(); }
+};
 
 int ensure_pin(ldt_ctx *c, PinBuf &b, size_t need) {
   if (b.cap >= need) return LDT_OK;
@@ -277,6 +365,21 @@ int ensure_pin(ldt_ctx *c, PinBuf &b, size_t need) {
   if (hipHostMalloc(&b.p, cap, hipHostMallocDefault) != hipSuccess)
     return set_err(c, LDT_ERR_NOMEM, "hipHostMalloc(%zu) failed", cap);
   b.cap = cap;
+  return LDT_OK;
+}
+
+// Grow pinned slot `sl`'s buffer (`which` = h_data or h_plan) and, while it
+// is idle, the other slot's to the same size: a pinned allocation costs
+// milliseconds, so it should not wait for the first call on the other slot.
+int ensure_pin_slots(ldt_ctx *c, PinBuf (&bufs)[ldt_ctx::kSlots], int sl, size_t need) {
+  int rc;
+  if ((rc = ensure_pin(c, bufs[sl], need))) return rc;
+  for (int k = 0; k < ldt_ctx::kSlots; ++k) {
+    if (k == sl || bufs[k].cap >= need) continue;
+    if (c->slot_used[k] && hipEventQuery(c->slot_ev[k]) != hipSuccess) continue;
+    (void)hipGetLastError();
+    if ((rc = ensure_pin(c, bufs[k], need))) return rc;
+  }
   return LDT_OK;
 }
 
@@ -361,13 +464,39 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   DeviceGuard g(c->device);
   int rc;
   if ((rc = order_streams(c, s))) return rc;
-
-  // ---- parse headers ----
   HostTimer ht(c);
   const int64_t base = (int64_t)offsets[arr_offset];
   const int64_t total_bytes = (int64_t)offsets[arr_offset + n] - base;
   if (total_bytes < 0) return set_err(c, LDT_ERR_ARG, "offsets not monotonic");
   const uint8_t *cells_host = data_host + base; // cell i at cells_host + (offsets[i] - base)
+  if (c->coef_dirty) {
+    // an earlier call failed between the Huffman and IDCT launches
+    if (c->d_coef.p) HIPCHK(c, hipMemsetAsync(c->d_coef.p, 0, c->d_coef.cap, s));
+    c->coef_dirty = false;
+  }
+
+  // ---- pinned slot, then the cells' copy into it on the pool threads: the
+  // header walk below overlaps it (the copy is joined before the H2D) ----
+  if ((rc = acquire_slot(c))) return rc;
+  const int sl = c->slot;
+  std::shared_ptr<HostRange> reg; // registered range the H2D reads from
+  CopyJoin cj;
+  if (!data_dev && total_bytes > 0) {
+    reg = host_acquire(cells_host, (size_t)total_bytes, c->device);
+    if (!reg) {
+      if ((rc = ensure_pin_slots(c, c->h_data, sl, (size_t)total_bytes + 16))) return rc;
+      CopyPool &pool = copier(c);
+      pool.start(c->h_data[sl].p, cells_host, (size_t)total_bytes);
+      cj.p = &pool;
+    }
+  }
+  struct RegRelease {
+    std::shared_ptr<HostRange> &r;
+    ~RegRelease() { host_release(r); }
+  } reg_release{reg};
+  ht.mark(kHpSlot);
+
+  // ---- parse headers ----
   std::vector<ImgPlan> P((size_t)n);
   std::vector<ImgDesc> D((size_t)n);
   std::vector<Segment> S;
@@ -655,7 +784,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     if (kv > max_ks_v) max_ks_v = kv;
   }
 
-  ht.mark(0); // headers parsed, per-image plans built
+  ht.mark(kHpParse); // headers parsed, per-image plans built
   // ---- plan blob layout ----
   PlanHdr ph;
   memset(&ph, 0, sizeof(ph));
@@ -698,10 +827,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   ph.max_blocks = max_blocks;
   ph.total_blocks = coef_blocks;
 
-  if ((rc = acquire_slot(c))) return rc;
-  ht.mark(1); // pinned slot free
-  const int sl = c->slot;
-  if ((rc = ensure_pin(c, c->h_plan[sl], (size_t)plan_bytes))) return rc;
+  if ((rc = ensure_pin_slots(c, c->h_plan, sl, (size_t)plan_bytes))) return rc;
   uint8_t *hp = static_cast<uint8_t *>(c->h_plan[sl].p);
   memcpy(hp, &ph, sizeof(ph));
   memcpy(hp + ph.off_desc, D.data(), sizeof(ImgDesc) * (size_t)n);
@@ -730,36 +856,25 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if ((rc = ensure_dev(c, c->d_dcv, (size_t)coef_blocks * 2 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dscnt, 16 * (size_t)(n_chunks + 1), s))) return rc;
-  ht.mark(2); // plan blob written, buffers sized
-  auto tick = [&](int k, std::chrono::steady_clock::time_point &t0) {
-    const auto t1 = std::chrono::steady_clock::now();
-    if (ht.on) c->host_us[k] += std::chrono::duration<double, std::micro>(t1 - t0).count();
-    t0 = t1;
-  };
-  auto t0 = std::chrono::steady_clock::now();
+  ht.mark(kHpPlan); // plan blob written, buffers sized
   prof_begin(c, LDT_STAGE_H2D, s);
-  tick(8, t0);
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
     if ((rc = ensure_dev(c, c->d_data, (size_t)total_bytes + 16, s))) return rc;
-    if (total_bytes > 0 && host_registered(cells_host, (size_t)total_bytes)) {
-      // page-locked in place: DMA straight from the caller's pages
-      HIPCHK(c, hipMemcpyAsync(c->d_data.p, cells_host, (size_t)total_bytes, hipMemcpyHostToDevice, s));
-    } else {
-      if ((rc = ensure_pin(c, c->h_data[sl], (size_t)total_bytes + 16))) return rc;
-      pinned_copy(c, c->h_data[sl].p, cells_host, (size_t)total_bytes);
-      HIPCHK(c, hipMemcpyAsync(c->d_data.p, c->h_data[sl].p, (size_t)total_bytes,
-                               hipMemcpyHostToDevice, s));
+    if (total_bytes > 0) {
+      // registered: DMA straight from the caller's pages; else from the slot
+      cj.wait();
+      HIPCHK(c, hipMemcpyAsync(c->d_data.p, reg ? (const void *)cells_host : c->h_data[sl].p,
+                               (size_t)total_bytes, hipMemcpyHostToDevice, s));
+      host_release(reg);
     }
     dev_cells = static_cast<const uint8_t *>(c->d_data.p);
   }
-  tick(6, t0);
   HIPCHK(c, hipMemcpyAsync(c->d_plan.p, hp, (size_t)plan_bytes, hipMemcpyHostToDevice, s));
-  tick(7, t0);
   HIPCHK(c, hipEventRecord(c->slot_ev[sl], s));
   c->slot_used[sl] = true;
   prof_mark(c, LDT_STAGE_H2D, s);
-  tick(7, t0);
+  ht.mark(kHpCopy);
 
   uint8_t *dp = static_cast<uint8_t *>(c->d_plan.p);
   DevPlan p;
@@ -786,6 +901,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     p.win_bytes = (int)(std::min<int64_t>(max_window, cap) & ~(int64_t)15);
   }
   p.warm_pct = c->warm_pct;
+  p.resize_waves_pct = c->resize_waves_pct;
+  p.resize420 = c->resize_impl == 0 ? 1 : 0;
   p.n_chunks = n_chunks;
   p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
   p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
@@ -805,15 +922,16 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
   w.ds_cnt = static_cast<int4 *>(c->d_dscnt.p);
 
-  ht.mark(3); // copies enqueued
   HIPCHK(c, launch_destuff(p, w, s));
   prof_mark(c, LDT_STAGE_DESTUFF, s);
+  c->coef_dirty = true; // until k_idct is enqueued behind the Huffman output
   HIPCHK(c, launch_huff_parallel(p, w, s));
   HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_prog(p, w, s));
   HIPCHK(c, launch_dc_scan(p, w, s));
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
   HIPCHK(c, launch_idct(p, w, s));
+  c->coef_dirty = false;
   prof_mark(c, LDT_STAGE_IDCT, s);
   {
     // k_resize4 writes the failed images itself; the streaming fallback does not
@@ -827,7 +945,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   prof_mark(c, LDT_STAGE_RESIZE, s);
   c->cur_ev = nullptr;
 
-  ht.mark(4); // kernels launched
+  ht.mark(kHpLaunch); // kernels launched
   // ---- per-image status back to the host ----
   if ((size_t)n > c->h_status_cap) {
     if (c->h_status) HIPCHK(c, hipHostFree(c->h_status));
@@ -839,7 +957,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   HIPCHK(c, hipMemcpyAsync(c->h_status, w.status, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
   c->last_n = n;
   if ((rc = finish_call(c, s))) return rc;
-  ht.mark(5); // status copy enqueued
+  ht.mark(kHpStatus); // status copy enqueued
   memcpy(status_out, st.data(), 4 * (size_t)n);
   if (c->sync_status) {
     HIPCHK(c, hipStreamSynchronize(s));
@@ -921,22 +1039,36 @@ int ldt_register_host(ldt_ctx *c, const void *ptr, size_t len) {
     (void)hipGetLastError();
     return set_err(c, LDT_ERR_HIP, "hipHostRegister(%zu bytes): %s", len, hipGetErrorString(e));
   }
+  auto r = std::make_shared<HostRange>();
+  r->lo = (uintptr_t)ptr;
+  r->hi = (uintptr_t)ptr + len;
   std::lock_guard<std::mutex> l(g_host_m);
-  g_host_ranges.push_back({(uintptr_t)ptr, (uintptr_t)ptr + len});
+  g_host_ranges.push_back(std::move(r));
   return LDT_OK;
 }
 
 int ldt_unregister_host(ldt_ctx *c, const void *ptr) {
   if (!c) return LDT_ERR_ARG;
   DeviceGuard g(c->device);
+  uint64_t devmask;
   {
-    std::lock_guard<std::mutex> l(g_host_m);
+    // no new decode picks the range up once it is out of the list; wait for
+    // the ones that did until they have enqueued their copies
+    std::unique_lock<std::mutex> l(g_host_m);
     auto it = std::find_if(g_host_ranges.begin(), g_host_ranges.end(),
-                           [&](const HostRange &r) { return r.lo == (uintptr_t)ptr; });
+                           [&](const std::shared_ptr<HostRange> &r) { return r->lo == (uintptr_t)ptr; });
     if (it == g_host_ranges.end()) return set_err(c, LDT_ERR_ARG, "unregister: range not registered");
+    std::shared_ptr<HostRange> r = *it;
     g_host_ranges.erase(it);
+    g_host_cv.wait(l, [&] { return r->inflight == 0; });
+    devmask = r->devmask;
   }
-  HIPCHK(c, hipDeviceSynchronize()); // no copy from the range is still in flight
+  // every device that copied from the range has finished doing so
+  for (int d = 0; d < 64; ++d) {
+    if (!((devmask >> d) & 1)) continue;
+    DeviceGuard gd(d);
+    HIPCHK(c, hipDeviceSynchronize());
+  }
   HIPCHK(c, hipHostUnregister(const_cast<void *>(ptr)));
   return LDT_OK;
 }
@@ -959,13 +1091,27 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     c->warm_pct = (int)value;
     return LDT_OK;
   case LDT_OPT_RESIZE_IMPL:
-    if (value != 0 && value != 2) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
+    if (value < 0 || value > 2) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
     c->resize_impl = (int)value;
     return LDT_OK;
   case LDT_OPT_SUBSEQ_BITS:
     if (value < 64 || value > 8192 || (value & 31))
       return set_err(c, LDT_ERR_ARG, "subsequence bits %lld", (long long)value);
     c->subseq_bits = (int)value;
+    return LDT_OK;
+  case LDT_OPT_COPY_THREADS:
+    if (value < -1 || value > 31) return set_err(c, LDT_ERR_ARG, "copy threads %lld", (long long)value);
+    if ((int)value != c->copy_threads) {
+      c->copy_threads = (int)value;
+      c->copier.reset(); // rebuilt with the new size on the next copy
+    }
+    return LDT_OK;
+  case LDT_OPT_HOST_TIMING:
+    c->host_timing = value != 0;
+    return LDT_OK;
+  case LDT_OPT_RESIZE_WAVES_PCT:
+    if (value < 10 || value > 1000) return set_err(c, LDT_ERR_ARG, "resize waves %lld%%", (long long)value);
+    c->resize_waves_pct = (int)value;
     return LDT_OK;
   default:
     return set_err(c, LDT_ERR_ARG, "unknown option %d", option);
@@ -1001,6 +1147,17 @@ int ldt_decode_batch_resident(ldt_ctx *c, const uint8_t *data_host, const uint8_
   return decode_core<int64_t>(c, data_host, data_dev, offsets, 0, n, nullptr, labels, 0,
                               out_img_dev, out_lbl_dev, norm, (hipStream_t)stream,
                               per_image_status);
+}
+
+int ldt_host_times(ldt_ctx *c, double *us_out, int64_t *calls_out, int reset) {
+  if (!c) return LDT_ERR_ARG;
+  for (int k = 0; k < kHpCount; ++k) {
+    if (us_out) us_out[k] = c->host_us[k];
+    if (reset) c->host_us[k] = 0;
+  }
+  if (calls_out) *calls_out = c->host_calls;
+  if (reset) c->host_calls = 0;
+  return LDT_OK;
 }
 
 int ldt_stage_times(ldt_ctx *c, double *ms_out, int64_t *count_out, int reset) {

@@ -270,11 +270,13 @@ __device__ __forceinline__ uint32_t lookup(const Dec &dec, const St &st, uint32_
 }
 
 // HUFF_EXTEND of the s magnitude bits following the code.
+// raw < 2^(s-1) (top magnitude bit clear) is negative: raw - (2^s - 1); the
+// s-bit mask is one v_bfm (s = 0: raw = mask = 0, value 0).
 __device__ __forceinline__ int ext_value(uint32_t pk, uint32_t e) {
   const uint32_t total = e & 31, s = (e >> 5) & 15;
   const int raw = (int)__builtin_amdgcn_ubfe(pk, 32 - total, s);
-  const int half = (1 << s) >> 1;
-  return raw < half ? raw - 2 * half + 1 : raw;
+  const int mask = (int)((1u << s) - 1u);
+  return raw <= (mask >> 1) ? raw - mask : raw;
 }
 
 // k += adv; k >= 64 ends the block (EOB advances by 64).
@@ -323,77 +325,60 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
 // 1..63 (DC lives in dcv); k_idct de-zigzags while dequantising. Slots are
 // combined 8 at a time (16 bytes) in registers and written with one store per
 // touched group instead of one 2-byte scatter per coefficient: a block's
-// coefficient indices only grow, so a group is complete once the index leaves
-// it or the block ends. Groups a neighbouring range may also write (a block
-// straddling the range boundary) are written slot by slot.
+// coefficient indices only grow, so a group is complete once the decode
+// moves to another group or block.
 __device__ __forceinline__ void store_group(uint4 *__restrict__ p, uint64_t lo, uint64_t hi) {
   *p = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-// Coefficient-writing decode of one range: from the reader's position until
-// it reaches `stop` or the segment's `total` blocks are complete. cursor is
-// the current block (segment-relative, -1 before the first DC). DC symbols
-// store their difference in dcv_seg[cursor] (dc_scan_image adds the predictors);
-// nonzero AC coefficients go to the image's group planes (block
-// seg_blk0 + cursor of coef_img, see coef_piece), which are all zero
-// beforehand (k_idct clears every block it reads). The loop body is straight-line: every
-// store is predicated, so a wave branches only around stores no lane makes.
+// Coefficient-writing decode of one range, with block ownership: a block
+// belongs to the range that decodes its DC symbol. The run starts at the
+// reader's position with cursor -1; a block it enters mid-way (k != 0) is
+// decoded without stores (the previous range writes it), and the run goes on
+// past `stop` until its last block is complete (k back to 0), so every block
+// is written by one lane and no group is shared between lanes. Blocks are
+// base + cursor of the image for cursor in [0, lim) (lim: the segment's
+// blocks not started before the range); the run ends before a block beyond
+// lim. Every value goes into the buffered group at its zigzag slot: the DC
+// difference into slot 0 (the DC predictor scan reads it from group plane 0
+// and writes the absolute DC to dcv; k_idct takes the DC from dcv), nonzero
+// AC coefficients into slots 1..63 of the image's group planes (block
+// base + cursor of coef_img, see coef_piece), which are all zero beforehand
+// (k_idct clears every block it reads). A zero value (EOB, ZRL, a zero DC
+// difference) changes nothing. The loop's one store site flushes the buffered
+// group when a nonzero value opens another (block, group) key; the partial
+// block a run enters has negative keys and is never stored.
 template <class W>
 __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
-                                          int &cursor, int total, uint4 *__restrict__ coef_img,
-                                          int seg_blk0, int npad, int16_t *__restrict__ dcv_seg) {
+                                          int &cursor, int lim, uint4 *__restrict__ coef_img,
+                                          int base, int npad) {
   uint64_t lo = 0, hi = 0; // buffered group: slots 0-3, 4-7
-  int grp = -1;            // its index (slot >> 3), -1 = empty
-  // entered mid-block: the previous range may have written this group of it
-  const int shared_g = st.k != 0 ? (st.k >> 3) : -1;
-  bool first = true;       // still in the block the range entered
-  bool go = R.p < stop && !(st.k == 0 && cursor + 1 >= total);
+  int ckey = -1;           // its (cursor << 3) | group; < 0: none
+  bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   while (go) {
-    const bool dc = st.k == 0;
-    cursor += dc ? 1 : 0;
-    // corrupt streams can count more blocks than the segment has, so a range
-    // may enter mid-block with its cursor outside [0, total): no stores then
-    const bool inb = (uint32_t)cursor < (uint32_t)total;
+    cursor += st.k == 0 ? 1 : 0;
     const uint32_t pk = R.peek();
     const uint32_t e = lookup(dec, st, pk);
     const int v = ext_value(pk, e);
     const int adv = (int)(e >> 9);
-    const bool nz = !dc && ((e >> 5) & 15) != 0;
     // a corrupt stream can run k past 63 (a run or ZRL from k > 48): jdhuff.c
-    // then stores into natural[k >= 64] = position 63; so does this clamp
-    // (and it keeps the store inside the block's eight groups)
+    // then stores into natural[k >= 64] = position 63; so does this clamp.
+    // A DC symbol (k = 0, advance 1) lands in slot 0.
     const int slot = min(st.k + adv - 1, 63);
-    const int g = slot >> 3;
-    // the block's groups in the image's group planes (coef_piece)
-    const int ib = seg_blk0 + cursor;
-    if (dc) dcv_seg[cursor] = (int16_t)v;
-    const bool direct = nz && first && g == shared_g;
-    if (direct && inb) reinterpret_cast<int16_t *>(coef_img + coef_piece(ib, g, npad))[slot & 7] = (int16_t)v;
-    const bool buf = nz && !direct;
-    const bool newg = buf && g != grp;
-    if (newg && grp >= 0 && inb) store_group(coef_img + coef_piece(ib, grp, npad), lo, hi);
-    lo = newg ? 0ull : lo;
-    hi = newg ? 0ull : hi;
-    grp = newg ? g : grp;
-    const uint64_t x = buf ? (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3)) : 0ull;
+    const int gkey = (cursor << 3) | (slot >> 3); // cursor -1: negative
+    const bool open = v != 0 && gkey != ckey;
+    if (open && ckey >= 0) store_group(coef_img + coef_piece(base + (ckey >> 3), ckey & 7, npad), lo, hi);
+    lo = open ? 0ull : lo;
+    hi = open ? 0ull : hi;
+    ckey = open ? gkey : ckey;
+    const uint64_t x = (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3));
     lo |= (slot & 4) ? 0ull : x;
     hi |= (slot & 4) ? x : 0ull;
     R.consume((int)(e & 31));
-    const bool end = st.k + adv >= 64;
-    if (end && grp >= 0 && inb) store_group(coef_img + coef_piece(ib, grp, npad), lo, hi);
-    grp = end ? -1 : grp;
-    first = first && !end;
     advance(st, dec, adv);
-    go = R.p < stop && !(st.k == 0 && cursor + 1 >= total);
+    go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   }
-  if (grp >= 0 && (uint32_t)cursor < (uint32_t)total) { // the open block continues in the next range
-    int16_t *p = reinterpret_cast<int16_t *>(coef_img + coef_piece(seg_blk0 + cursor, grp, npad));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint16_t x = (uint16_t)(((j & 4) ? hi : lo) >> (16 * (j & 3)));
-      if (x) p[j] = (int16_t)x;
-    }
-  }
+  if (ckey >= 0) store_group(coef_img + coef_piece(base + (ckey >> 3), ckey & 7, npad), lo, hi);
 }
 
 // ---------------------------------------------------------------------------
@@ -425,8 +410,8 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
     int cursor = -1;
     const int blk0 = sg.mcu_first * d.bpm; // image-relative
     // a valid segment ends inside its bits; 64 bits of slack bound a corrupt one
-    write_run(R, st, dec, pbias + seg_bits + 64, cursor, total,
-              reinterpret_cast<uint4 *>(coef + d.coef_off * 64), blk0, coef_npad(d), dcv + d.coef_off + blk0);
+    write_run(R, st, dec, pbias + seg_bits + 64, cursor, total, reinterpret_cast<uint4 *>(coef + d.coef_off * 64),
+              blk0, coef_npad(d));
     if (R.p - pbias > seg_bits || cursor + 1 < total || st.k != 0) status[img] = 3; // truncated
   }
 }
@@ -443,11 +428,12 @@ hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s)
 // DC predictors (jdhuff.c: last_dc_val[ci] += diff, reset to 0 at every
 // restart marker, process_restart) of one image, by its NT-thread workgroup:
 // thread t owns a run of consecutive blocks; a segmented scan over the threads
-// carries the per-component sums. Stores the absolute DC (JCOEF, truncated) in
-// place. `scr` is 4*NT/64 ints of LDS; contains __syncthreads.
+// carries the per-component sums. The DC differences are read from slot 0 of
+// group plane 0 (write_run), the absolute DC (JCOEF, truncated) is stored in
+// v. `scr` is 4*NT/64 ints of LDS; contains __syncthreads.
 template <int NT>
-__device__ __forceinline__ void dc_scan_image(const ImgDesc &d, int16_t *__restrict__ v,
-                                              LDS_AS int32_t *scr) {
+__device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint4 *__restrict__ plane0,
+                                              int16_t *__restrict__ v, LDS_AS int32_t *scr) {
   static_assert(NT % 64 == 0, "whole waves");
   const int tid = threadIdx.x;
   const int bpm = d.bpm;
@@ -473,7 +459,7 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, int16_t *__restr
         flag = 1;
       }
       const int c = (int)((compmap >> (2 * b)) & 3);
-      const int dv = v[x];
+      const int dv = *reinterpret_cast<const int16_t *>(plane0 + x);
       s0 += c == 0 ? dv : 0;
       s1 += c == 1 ? dv : 0;
       s2 += c == 2 ? dv : 0;
@@ -525,7 +511,7 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, int16_t *__restr
   for (int64_t x = lo; x < hi; ++x) {
     if (sp == 0) r0 = r1 = r2 = 0;
     const int c = (int)((compmap >> (2 * b)) & 3);
-    const int dv = v[x];
+    const int dv = *reinterpret_cast<const int16_t *>(plane0 + x);
     r0 += c == 0 ? dv : 0;
     r1 += c == 1 ? dv : 0;
     r2 += c == 2 ? dv : 0;
@@ -538,18 +524,20 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, int16_t *__restr
 // k_dc_scan: the DC predictors of the serial decoder's images (the parallel
 // decoder's workgroups scan their own image after the write pass).
 __global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ descs,
+                                                 const int16_t *__restrict__ coef,
                                                  int16_t *__restrict__ dcv,
                                                  const int32_t *__restrict__ status) {
   __shared__ int32_t scr[4 * 256 / 64];
   const int img = blockIdx.x;
   // progressive: dcv holds the final DC; sub_bits > 0: k_huff_image
   if (status[img] != 0 || descs[img].nseg == 0 || descs[img].sub_bits > 0) return;
-  dc_scan_image<256>(descs[img], dcv + descs[img].coef_off, (LDS_AS int32_t *)scr);
+  dc_scan_image<256>(descs[img], reinterpret_cast<const uint4 *>(coef + descs[img].coef_off * 64),
+                     dcv + descs[img].coef_off, (LDS_AS int32_t *)scr);
 }
 
 hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_serial == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dc_scan, dim3(p.n), dim3(256), 0, s, p.descs, w.dcv, w.status);
+  hipLaunchKernelGGL(k_dc_scan, dim3(p.n), dim3(256), 0, s, p.descs, w.coef, w.dcv, w.status);
   return hipGetLastError();
 }
 
@@ -929,16 +917,19 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   // ---- write pass from the true entry ----
   bool trunc = false;
   if (live) {
-    int cursor = pre - sh.ex_p[sh.seg_first[g.si]] - 1; // segment-relative block, -1 before the DC
+    // blocks of the segment started before this range: the first block whose
+    // DC this range decodes is the segment's block `bstart`
+    const int bstart = pre - sh.ex_p[sh.seg_first[g.si]];
     const int total = sg.mcu_count * d.bpm;
-    const int blk0 = sg.mcu_first * d.bpm; // image-relative
+    const int base = sg.mcu_first * d.bpm + bstart; // image-relative
+    int cursor = -1;
     St st = make_state(wbk);
     Rd<W> R;
     R.src = src;
     R.seek(g.pbias + wp);
-    write_run(R, st, dec, wstop, cursor, total, reinterpret_cast<uint4 *>(coef + d.coef_off * 64), blk0,
-              coef_npad(d), dcv + d.coef_off + blk0);
-    if (g.j == sg.sub_count - 1 && cursor + 1 < total) {
+    write_run(R, st, dec, wstop, cursor, total - bstart, reinterpret_cast<uint4 *>(coef + d.coef_off * 64),
+              base, coef_npad(d));
+    if (g.j == sg.sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;
     }
@@ -961,7 +952,8 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   // ---- DC predictors (the serial path runs k_dc_scan instead) ----
   if (!trunc) {
     __syncthreads(); // sh is free from here: its first 256 bytes are the scan scratch
-    dc_scan_image<kHuffThreads>(d, dcv + d.coef_off, (LDS_AS int32_t *)&sh);
+    dc_scan_image<kHuffThreads>(d, reinterpret_cast<const uint4 *>(coef + d.coef_off * 64), dcv + d.coef_off,
+                                (LDS_AS int32_t *)&sh);
   }
 }
 

@@ -43,14 +43,18 @@ OPT_SUBSEQ_BITS = 3
 OPT_PROFILE = 4
 OPT_RESIZE_IMPL = 5
 OPT_SYNC_WARM = 7
+OPT_COPY_THREADS = 8
+OPT_HOST_TIMING = 9
+OPT_RESIZE_WAVES_PCT = 10
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
+HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status")
 
 # Every symbol include/ldt.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "ldt_create", "ldt_destroy", "ldt_last_error", "ldt_set_option", "ldt_version",
     "ldt_decode_batch", "ldt_decode_batch_large", "ldt_decode_batch_resident",
-    "ldt_register_host", "ldt_unregister_host", "ldt_fetch_status", "ldt_stage_times", "ldt_resize_raw", "ldt_shard_ranges",
+    "ldt_register_host", "ldt_unregister_host", "ldt_fetch_status", "ldt_stage_times", "ldt_host_times", "ldt_resize_raw", "ldt_shard_ranges",
     "ldt_shard_fragments", "ldt_distributed_indices",
 )
 
@@ -116,6 +120,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_decode_batch_resident.argtypes = [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
         L.ldt_fetch_status.argtypes = [vp, vp, vp, i64]
         L.ldt_stage_times.argtypes = [vp, vp, vp, i32]
+        L.ldt_host_times.argtypes = [vp, vp, vp, i32]
         L.ldt_resize_raw.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, vp, vp]
         L.ldt_shard_ranges.argtypes = [vp, i64, i64, i32, i32, vp, i64, vp, vp]
         L.ldt_shard_fragments.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, i64, vp, vp, vp]
@@ -127,7 +132,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_unregister_host.argtypes = [vp, vp]
         for name in ("ldt_set_option", "ldt_decode_batch", "ldt_decode_batch_large", "ldt_register_host",
                      "ldt_unregister_host",
-                     "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_resize_raw", "ldt_stage_times",
+                     "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_resize_raw", "ldt_stage_times", "ldt_host_times",
                      "ldt_shard_ranges", "ldt_shard_fragments", "ldt_distributed_indices",
                      "ldt_debug_resample_coeffs",
                      "ldt_debug_counters"):
@@ -165,6 +170,16 @@ class Context:
         self.check(self.lib.ldt_stage_times(self.handle, ms.ctypes.data, cnt.ctypes.data, int(reset)),
                    "ldt_stage_times")
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(STAGES)}
+
+    def host_times(self, reset: bool = False):
+        """({phase: total_us}, calls) from LDT_OPT_HOST_TIMING."""
+        import numpy as np
+
+        us = np.zeros(len(HOST_PHASES), np.float64)
+        calls = ctypes.c_int64(0)
+        self.check(self.lib.ldt_host_times(self.handle, us.ctypes.data, ctypes.byref(calls), int(reset)),
+                   "ldt_host_times")
+        return {k: float(us[i]) for i, k in enumerate(HOST_PHASES)}, int(calls.value)
 
     def __del__(self):
         h = getattr(self, "handle", None)

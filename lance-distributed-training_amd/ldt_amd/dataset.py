@@ -193,9 +193,15 @@ class LanceDataset(IterableDataset):
         # the process group (pad=True's all_reduce) live, and the workers only
         # read rows. Each worker w then yields plan batches w, w+nw, ... in
         # order, which the DataLoader's round-robin turns back into the
-        # sampler's order.
+        # sampler's order. A sampler without a read plan (any object following
+        # the pylance protocol sampler(dataset, batch_size=...)) runs in the
+        # workers instead.
+        if self.filter is not None:
+            raise NotImplementedError("filter is not supported by the dataset shim")
         state = dict(self.__dict__)
-        state["_worker_plan"] = self._sampler().read_plan(self.dataset, self.batch_size)
+        sampler = self._sampler()
+        if hasattr(sampler, "read_plan"):
+            state["_worker_plan"] = sampler.read_plan(self.dataset, self.batch_size)
         return state
 
     def __iter__(self):
@@ -206,9 +212,23 @@ class LanceDataset(IterableDataset):
         info = get_worker_info()
         fn = self.to_tensor_fn
         if info is not None:
+            if self.filter is not None:
+                raise NotImplementedError("filter is not supported by the dataset shim")
             plan = getattr(self, "_worker_plan", None)
-            if plan is None:  # not pickled (fork start method): plan in the worker
-                plan = self._sampler().read_plan(self.dataset, self.batch_size)
+            sampler = self._sampler()
+            if plan is None and hasattr(sampler, "read_plan"):
+                # not pickled (fork start method): this build's samplers plan on
+                # the GPU (and pad=True runs a collective), which a forked child
+                # must not touch
+                raise RuntimeError("LanceDataset workers need multiprocessing_context='spawn' with this "
+                                   "build's samplers (the batch plan runs device kernels in the main process)")
+            if plan is None:
+                batches = sampler(self.dataset, batch_size=self.batch_size, columns=self.columns,
+                                  batch_readahead=self.batch_readahead)
+                for k, rb in enumerate(batches):
+                    if k % info.num_workers == info.id:
+                        yield fn(rb) if fn is not None else rb
+                return
             for desc in plan[info.id::info.num_workers]:
                 rb = read_planned(self.dataset, desc, self.columns)
                 yield fn(rb) if fn is not None else rb

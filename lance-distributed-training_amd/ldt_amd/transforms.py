@@ -633,6 +633,21 @@ class DecodePipeline:
                 tot[k] = (a[0] + ms, a[1] + n)
         return tot
 
+    def host_times(self, reset: bool = False):
+        """Host phase times summed over the slots' contexts (LDT_OPT_HOST_TIMING)."""
+        tot: dict = {}
+        calls = 0
+        for c in self.ctxs:
+            us, n = c.host_times(reset=reset)
+            calls += n
+            for k, v in us.items():
+                tot[k] = tot.get(k, 0.0) + v
+        return tot, calls
+
+    def set_option(self, opt: int, value: int):
+        for c in self.ctxs:
+            c.set_option(opt, value)
+
     def _slot_status(self, i: int) -> dict:
         c, s, n = self.ctxs[i], self.streams[i], self.sizes[i]
         if n == 0:
@@ -659,7 +674,7 @@ class DecodePipeline:
 
 
 def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int = 0,
-                      register: bool = False, **fixed):
+                      register: bool = False, register_cap: int = 8, **fixed):
     """A pipelined ``to_tensor_fn`` for ``LanceDataset(..., to_tensor_fn=...)``
     (lance_iterable.py:53-59): each call enqueues its RecordBatch on one of
     `depth` contexts/streams and returns at once, so batch k+1's host copy and
@@ -676,13 +691,39 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
     buffer page-locks that whole buffer in place (``register_host``), so the
     batches sliced from a memory-mapped fragment reach HBM by DMA without a
     host memcpy. Only for long-lived buffers (a mapped dataset), not for
-    batches built anew each step."""
+    batches built anew each step. At most ``register_cap`` buffers stay
+    registered by this function (least recently used ones are unregistered),
+    and a buffer the driver refuses to lock (memlock limit, overlapping
+    registration) switches the function to the copying path instead of
+    raising (ldt.h: such a range stays on the copying path)."""
+    from collections import OrderedDict
+
     pipe = DecodePipeline(depth=depth, device=device)
     image_column = fixed.get("image_column", "image")
+    owned: "OrderedDict[int, object]" = OrderedDict()  # registrations made here, LRU order
+    reg_on = [bool(register)]
 
     def maybe_register(batch, col):
-        if register and isinstance(batch, pa.RecordBatch):
-            register_host(_column(batch, col), device=device)
+        if not reg_on[0] or not isinstance(batch, pa.RecordBatch):
+            return
+        arr = _column(batch, col)
+        addr, size = _host_range(arr)
+        if size == 0:
+            return
+        if addr in owned:
+            owned.move_to_end(addr)
+            return
+        if addr in _registered:  # registered by the caller: theirs to manage
+            return
+        try:
+            register_host(arr, device=device)
+        except _lib.LdtError:
+            reg_on[0] = False  # copying path from here on
+            return
+        owned[addr] = arr
+        while len(owned) > max(1, int(register_cap)):
+            _, old = owned.popitem(last=False)
+            unregister_host(old)
 
     def to_tensor_fn(batch, **kwargs):
         maybe_register(batch, kwargs.get("image_column", image_column))
@@ -693,8 +734,15 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
                                label_column=kwargs.get("label_column", fixed.get("label_column", "label")))
         return _as_device_batch(img, lbl)
 
+    def release():
+        """Unregister the buffers this function registered (waits for the device)."""
+        while owned:
+            _, old = owned.popitem(last=False)
+            unregister_host(old)
+
     to_tensor_fn.check = pipe.check
     to_tensor_fn.pipeline = pipe
+    to_tensor_fn.release = release
     to_tensor_fn.prefetch = max(0, min(int(prefetch), depth - 1))
     def registered(batches):
         for b in batches:

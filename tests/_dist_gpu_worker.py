@@ -6,7 +6,7 @@ import os
 import sys
 
 
-def run(rank, world, port, uri, outdir):
+def run(rank, world, port, uri, outdir, check_every=7):
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
     for p in (os.path.join(repo, "lance-distributed-training_amd"), repo, here):
@@ -33,7 +33,7 @@ def run(rank, world, port, uri, outdir):
     for k, b in enumerate(loader):
         lbl = b["label"].cpu().numpy()
         labels.append(lbl.tolist())
-        if k % 7 == 0:  # every 7th batch image by image vs the oracle
+        if k % check_every == 0:  # every check_every-th batch image by image vs the oracle
             rows = ds.take(lbl.tolist(), ["image"]).column("image").to_pylist()
             img = b["image"].cpu().numpy()
             for j, cell in enumerate(rows):

@@ -51,3 +51,45 @@ def test_two_ranks_fragment_sampler_pad_decode(tmp_path):
     assert not (seen[0] & seen[1]), "ranks share rows"
     assert sorted(seen[0] | seen[1]) == list(range(n)), "rows missing"
     assert r[0]["bad"] == [] and r[1]["bad"] == [], "decoded images differ from the oracle"
+
+
+FRAGS8 = [50] * 6 + [3]  # FOOD101's [12500 x 6, 750] scaled 1/250
+
+
+def test_eight_ranks_empty_rank_pad_decode(tmp_path):
+    """W = 8 over FOOD101's fragment shape (README.md:140-155: [98 x 6, 6, 0]
+    batches per rank): ranks 0-5 own a full fragment,
+    rank 6 the short one, rank 7 no rows. Eight gloo ranks on cuda:0 plan with
+    the device shard kernel and agree on the padded count with one
+    all_reduce(MAX): every rank yields it, the ranks' own (unpadded) batches
+    partition the rows, the empty rank yields real rows, and every decoded
+    image is bit-exact against the oracle."""
+    import pyarrow as pa
+    import torch.multiprocessing as mp
+
+    import ldt_amd
+    import _dist_gpu_worker
+    from ldt_amd import synth
+
+    n = sum(FRAGS8)
+    cells = [synth.encode(synth.field(40 + (i % 5) * 8, 48 + (i % 3) * 8, 7000 + i, 6.0)) for i in range(n)]
+    uri = str(tmp_path / "food_w8")
+    ldt_amd.write_dataset(
+        pa.table({"image": pa.array(cells, pa.binary()), "label": pa.array(np.arange(n, dtype=np.int64))}),
+        uri, max_rows_per_file=50)
+    assert [f.count_rows() for f in ldt_amd.dataset(uri).get_fragments()] == FRAGS8
+    W = 8
+    mp.start_processes(_dist_gpu_worker.run, args=(W, _free_port(), uri, str(tmp_path), 1), nprocs=W,
+                       join=True, start_method="spawn")
+    r = [json.load(open(tmp_path / f"gpu_rank{k}.json")) for k in range(W)]
+    per_frag = [-(-f // B) for f in FRAGS8]      # 7 x 6, 1
+    local = [per_frag[k] if k < len(FRAGS8) else 0 for k in range(W)]
+    assert local == [7, 7, 7, 7, 7, 7, 1, 0]
+    assert all(x["batches"] == max(local) for x in r), [x["batches"] for x in r]
+    own = [set(v for b in r[k]["labels"][:local[k]] for v in b) for k in range(W)]
+    for a in range(W):
+        for b in range(a + 1, W):
+            assert not (own[a] & own[b]), f"ranks {a} and {b} share rows"
+    assert sorted(set().union(*own)) == list(range(n)), "rows missing"
+    assert r[7]["labels"] and all(0 <= v < n for b in r[7]["labels"] for v in b), "empty rank yields no rows"
+    assert all(x["bad"] == [] for x in r), "decoded images differ from the oracle"

@@ -374,8 +374,10 @@ def test_tall_bands_large_batches():
 
 
 def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
-    """The one-wave-per-band resize (default) and the banded workgroup kernel
-    (LDT_OPT_RESIZE_IMPL=2) give identical tensors on every golden image and on
+    """The default resize (k_resize420 with two waves per band for 4:2:0
+    sources, k_resize4 for the others), k_resize4 for all
+    (LDT_OPT_RESIZE_IMPL=1) and the banded workgroup kernel (=2) give
+    identical tensors on every golden image, on a c2/c1-shaped batch and on
     unaligned raw cells; a batch with a truncated image leaves no coefficient
     residue for the next batch (k_idct clears what the Huffman pass wrote)."""
     import torch
@@ -390,17 +392,22 @@ def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
     flat = np.concatenate([np.zeros(5, np.uint8), raw.reshape(-1)])
     arr = pa.array([flat[5 + k * raw[0].size: 5 + (k + 1) * raw[0].size].tobytes() for k in range(3)],
                    type=pa.binary(raw[0].size))
+    mixed = synth.q90_512(6, seed=8)[0] + synth.food101_like(10, seed=9)[0]
     res = {}
     try:
-        for impl in (0, 2):
+        for impl in (0, 1, 2):
             ctx.set_option(_lib.OPT_RESIZE_IMPL, impl)
             a = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
             b = ldt_amd.resize_raw(arr, 301, 517, normalize=True).cpu().numpy()
-            res[impl] = (a, b)
+            c = ldt_amd.decode_tensor_image(_batch(mixed))["image"].cpu().numpy()
+            res[impl] = (a, b, c)
     finally:
         ctx.set_option(_lib.OPT_RESIZE_IMPL, 0)
-    assert np.array_equal(res[0][0], res[2][0])
-    assert np.array_equal(res[0][1], res[2][1])
+    for impl in (1, 2):
+        for k in range(3):
+            assert np.array_equal(res[0][k], res[impl][k]), (impl, k)
+    for k in (0, 5, 6, 15):
+        _check(res[0][2][k], oracle.jpeg_to_tensor(mixed[k]), f"mixed[{k}]")
     for k in range(3):
         _check(res[0][1][k], oracle.raw_to_tensor(raw[k], normalize=True), f"raw301x517[{k}]")
     good = synth.encode(synth.field(384, 512, 11), quality=90)
@@ -479,6 +486,79 @@ def test_registered_host_buffer_bit_exact():
         ldt_amd.unregister_host(col)
     again = ldt_amd.decode_tensor_image(rb)["image"].cpu().numpy()
     assert np.array_equal(again, ref)
+
+
+def test_register_cap_and_refusal_fall_back_to_copy():
+    """make_to_tensor_fn(register=True, register_cap=1): each new buffer is
+    registered, the least recently used one unregistered (pinned memory stays
+    bounded), and a buffer the driver refuses to lock leaves the function on
+    the copying path instead of raising; every output stays bit-exact."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import synth, transforms
+
+    bs, refs = [], []
+    for k in range(3):
+        cells, labels = synth.food101_like(10, seed=300 + k)
+        rb = _batch(cells, labels)
+        bs.append(rb)
+        refs.append(ldt_amd.decode_tensor_image(rb)["image"].cpu().numpy())
+    before = set(transforms._registered)
+    fn = ldt_amd.make_to_tensor_fn(depth=2, register=True, register_cap=1)
+    outs = [fn(b) for b in bs + bs[:1]]
+    fn.check()
+    torch.cuda.synchronize()
+    assert len(set(transforms._registered) - before) <= 1
+    for o, ref in zip(outs, refs + refs[:1]):
+        assert np.array_equal(o["image"].cpu().numpy(), ref)
+    fn.release()
+    assert set(transforms._registered) == before
+    # a range the driver refuses to lock (memlock limit, overlap): the
+    # function stays on the copying path instead of raising
+    def refuse(obj, device=None):
+        raise ldt_amd.LdtError("ldt_register_host failed (rc=-2): hipHostRegister refused")
+
+    real = transforms.register_host
+    transforms.register_host = refuse
+    try:
+        fn2 = ldt_amd.make_to_tensor_fn(depth=2, register=True)
+        got = [fn2(b) for b in bs]
+        fn2.check()
+        for o, ref in zip(got, refs):
+            assert np.array_equal(o["image"].cpu().numpy(), ref)
+    finally:
+        transforms.register_host = real
+
+
+@pytest.mark.parametrize("threads", [0, 1, 7])
+def test_copy_pool_sizes_and_host_times(threads):
+    """LDT_OPT_COPY_THREADS: the cell copy into the pinned slot runs on 0 (the
+    caller alone), 1 or 7 pool threads while the caller walks the headers;
+    the decode is bit-exact for each (a 1 MB+ batch, so the pool path is
+    taken), and LDT_OPT_HOST_TIMING reports every phase per call."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    cells, labels = synth.q90_512(24, seed=41)
+    rb = _batch(cells, labels)
+    assert sum(len(c) for c in cells) > (1 << 20)
+    pipe = ldt_amd.DecodePipeline(depth=2)
+    pipe.set_option(_lib.OPT_COPY_THREADS, threads)
+    pipe.set_option(_lib.OPT_HOST_TIMING, 1)
+    outs = [pipe.decode(rb) for _ in range(4)]
+    pipe.check()
+    torch.cuda.synchronize()
+    us, calls = pipe.host_times(reset=True)
+    assert calls == 4 and set(us) == set(_lib.HOST_PHASES) and all(v >= 0 for v in us.values())
+    ref = outs[0][0].cpu().numpy()
+    for img, lbl in outs:
+        assert np.array_equal(img.cpu().numpy(), ref)
+        assert np.array_equal(lbl.cpu().numpy(), labels)
+    for k in (0, 11, 23):
+        _check(ref[k], oracle.jpeg_to_tensor(cells[k]), f"copy threads {threads}")
 
 
 @pytest.mark.parametrize("seed", range(3))

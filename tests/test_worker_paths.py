@@ -100,3 +100,48 @@ def test_iterable_lance_dataset_workers_yield_each_batch_once(cell_ds):
         got.append(lab.tolist())
         assert arr.to_pylist() == [cells[i // 3] for i in lab.tolist()]
     assert got == ref
+
+
+class _ProtocolSampler:
+    """A sampler that only follows the pylance call protocol
+    sampler(dataset, batch_size=...) -> RecordBatches (no read plan)."""
+
+    def __call__(self, dataset, *args, batch_size=128, columns=None, **kwargs):
+        for f in dataset.get_fragments():
+            yield from f.to_batches(batch_size, columns)
+
+
+def test_protocol_sampler_runs_in_spawn_workers(cell_ds):
+    """A sampler without this build's read plan still pickles with the
+    dataset; the workers run it and yield every batch once, in order."""
+    from ldt_amd import LanceDataset
+
+    ds, _ = cell_ds
+    ref = [rb.column(1).to_pylist() for rb in LanceDataset(ds, batch_size=6, sampler=_ProtocolSampler())]
+    lds = LanceDataset(ds, batch_size=6, sampler=_ProtocolSampler())
+    dl = DataLoader(lds, num_workers=3, batch_size=None, multiprocessing_context="spawn")
+    assert [rb.column(1).to_pylist() for rb in dl] == ref
+
+
+def test_filter_with_workers_raises(cell_ds):
+    """A filter the shim cannot apply must not be dropped silently in workers."""
+    import pickle
+
+    from ldt_amd import FullScanSampler, LanceDataset
+
+    ds, _ = cell_ds
+    lds = LanceDataset(ds, batch_size=6, sampler=FullScanSampler(), filter="label > 3")
+    with pytest.raises(NotImplementedError):
+        pickle.dumps(lds)
+
+
+def test_forked_worker_refuses_device_planning(cell_ds):
+    """Under fork the worker would run the device plan kernels (and pad=True's
+    collective) in the child: it raises instead."""
+    from ldt_amd import FullScanSampler, LanceDataset
+
+    ds, _ = cell_ds
+    lds = LanceDataset(ds, batch_size=6, sampler=FullScanSampler())
+    dl = DataLoader(lds, num_workers=1, batch_size=None, multiprocessing_context="fork")
+    with pytest.raises(RuntimeError, match="spawn"):
+        list(dl)
