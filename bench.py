@@ -75,6 +75,19 @@ def make_cells(workload: str, n: int, seed: int):
 # CPUs of the GPU box a one-GPU run may use (os.sched_getaffinity shows the
 # whole host there); LDT_CPU_SHARE overrides it on hosts with another share
 CPU_SHARE = int(os.environ.get("LDT_CPU_SHARE", "16"))
+# the per-GPU share of a whole 8-GPU node (256 host CPUs / 8), the CPU budget a
+# reference DataLoader per rank would have there
+NODE_SHARE_PER_GPU = 32
+
+
+def _cgroup_cpus():
+    """CPUs granted by the cgroup quota (cpu.max), or None when unlimited/unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(float(q) / float(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def _rates(times, imgs):
@@ -111,7 +124,7 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 7, workers=None):
     tmp = tempfile.mkdtemp(prefix="ldt_cpu_")
     host = len(os.sched_getaffinity(0))
     if workers is None:
-        workers = sorted({8, min(host, CPU_SHARE)})
+        workers = sorted({8, min(host, CPU_SHARE), min(host, NODE_SHARE_PER_GPU)})
     try:
         n = len(cells)
         lds.write_dataset(pa.table({"image": pa.array(cells, pa.binary()),
@@ -156,11 +169,16 @@ def cpu_baseline(cells, labels, batch: int = 128, reps: int = 7, workers=None):
         "sample": (f"the reference CPU path on this workload's cells: DataLoader(SafeLanceDataset shim, "
                    f"PIL collate_fn, batch {batch}, pin_memory, persistent spawn workers), "
                    f"{reps} x 2*num_workers timed batches per leg after warm-up; Pillow {pil_version} / "
-                   f"libjpeg-turbo {features.version_feature('libjpeg_turbo')}; host affinity {host} CPUs "
-                   f"(a one-GPU run may use {CPU_SHARE}; the whole-host leg is --cpu-workers {host}); "
-                   f"value = median of the num_workers={ref['num_workers']} leg (lance_map_style.py:137 default)"),
+                   f"libjpeg-turbo {features.version_feature('libjpeg_turbo')}; legs: num_workers 8 (the "
+                   f"reference default), {CPU_SHARE} (this box's CPU share for one GPU) and "
+                   f"{NODE_SHARE_PER_GPU} (one GPU's share of a 256-CPU 8-GPU node); host affinity {host} "
+                   f"CPUs (the whole-host leg, num_workers = len(os.sched_getaffinity(0)) per BASELINE.md "
+                   f"section 3, is --cpu-workers all: it exceeds a one-GPU run's CPU share on the shared "
+                   f"box); value = median of the num_workers={ref['num_workers']} leg "
+                   f"(lance_map_style.py:137 default)"),
         "legs": legs,
         "host_cpus": host,
+        "cgroup_cpus": _cgroup_cpus(),
         "cpu_share": CPU_SHARE,
         "torch_threads": torch.get_num_threads(),
     }
@@ -175,7 +193,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", default="",
-                    help="comma-separated num_workers legs of the CPU baseline (default: 8 and the CPU share)")
+                    help="comma-separated num_workers legs of the CPU baseline (default: 8, the CPU share and "
+                         "the per-GPU share of an 8-GPU node; 'all' = len(os.sched_getaffinity(0)))")
     ap.add_argument("--no-stage-events", action="store_true",
                     help="time without the per-stage HIP events (no roofline)")
     ap.add_argument("--depth", type=int, default=3,
@@ -184,6 +203,8 @@ def main():
                     help="batches per rank of one epoch of the dataset leg (0: skip the leg)")
     ap.add_argument("--dataset-epochs", type=int, default=2,
                     help="epochs in the dataset leg's timed region (each re-plans, as a training loop does)")
+    ap.add_argument("--resize-impl", type=int, default=0,
+                    help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize420 for 4:2:0; 1 k_resize4)")
     ap.add_argument("--registered", action="store_true",
                     help="also time the host leg with the cell buffers page-locked in place (ldt_register_host)")
     args = ap.parse_args()
@@ -267,6 +288,7 @@ def main():
         comp_bytes = float(np.mean([len(c) for c in cells_all]))
         it = [0]
         pipe = ldt_amd.DecodePipeline(depth=args.depth, device=dev, profile=not args.no_stage_events)
+        pipe.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
 
         def step():
             b = batches[it[0] % nb]
@@ -291,6 +313,7 @@ def main():
     def host_rate(bs, register=False):
         fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev, register=register)
         fn.pipeline.set_option(_lib.OPT_HOST_TIMING, 1)
+        fn.pipeline.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
         k = [0]
 
         def hstep():
@@ -327,6 +350,7 @@ def main():
     standalone = None
     if args.workload != "c5" and not args.no_stage_events:
         solo = ldt_amd.DecodePipeline(depth=1, device=dev, profile=True)
+        solo.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
         for k in range(3):
             solo.decode(batches[k % nb])
         barrier()
@@ -420,7 +444,8 @@ def main():
     if args.workload != "c5":
         res["config"]["compressed_bytes_per_img"] = round(comp_bytes, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "c5":
-        workers = [int(x) for x in args.cpu_workers.split(",") if x] or None
+        host_cpus = len(os.sched_getaffinity(0))
+        workers = sorted({host_cpus if x == "all" else int(x) for x in args.cpu_workers.split(",") if x}) or None
         res["cpu_baseline"] = cpu_baseline(cells_all, labels_all, workers=workers)
         res["gpu_over_cpu"] = {f"num_workers={leg['num_workers']}": round(value / leg["median"], 1)
                                for leg in res["cpu_baseline"]["legs"]}
@@ -452,6 +477,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     import pyarrow as pa
 
     import ldt_amd
+    from ldt_amd import _lib
 
     nbatch = args.dataset_batches
     # FOOD101's fragments [12500 x 6, 750] (create_datasets/classification.py:16,60)
@@ -483,6 +509,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     else:
         sampler = ldt_amd.ShardedBatchSampler(rank=rank, world_size=world)
     fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev)
+    fn.pipeline.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
     ds = ldt_amd.LanceDataset(path, batch_size=B, sampler=sampler, to_tensor_fn=fn)
 
     def epoch():

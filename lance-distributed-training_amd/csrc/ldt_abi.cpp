@@ -11,6 +11,7 @@
 // Replaces, per batch: lance_iterable.py:41-49 (to_pylist, PIL open/convert,
 // Resize, ToTensor, stack, label tensor) and lance_map_style.py:34-44.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -63,8 +64,14 @@ struct PinBuf {
 // chunk of the next one.
 class CopyPool {
 public:
-  explicit CopyPool(int nthreads) {
-    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this] { run(); });
+  // device: the HIP device the chunk DMAs are enqueued for (each pool thread
+  // selects it once)
+  CopyPool(int nthreads, int device) {
+    for (int i = 0; i < nthreads; ++i)
+      th_.emplace_back([this, device] {
+        (void)hipSetDevice(device);
+        run();
+      });
   }
   ~CopyPool() {
     {
@@ -76,9 +83,16 @@ public:
     for (auto &t : th_) t.join();
   }
   int threads() const { return (int)th_.size(); }
-  void start(void *dst, const void *src, size_t n) {
+  // Copy n bytes src -> dst (pinned). With dev_dst, every chunk is also
+  // enqueued as an H2D DMA dst -> dev_dst on `stream` as soon as its memcpy is
+  // done, so the PCIe transfer runs behind the host copy instead of after it;
+  // finish() returns once every chunk is copied and its DMA enqueued (all of
+  // them before anything the caller enqueues on `stream` afterwards).
+  void start(void *dst, const void *src, size_t n, void *dev_dst = nullptr, hipStream_t stream = nullptr) {
+    dma_err_ = hipSuccess;
     if (th_.empty() || n < ((size_t)1 << 20)) {
       memcpy(dst, src, n);
+      if (dev_dst) dma_err_ = hipMemcpyAsync(dev_dst, dst, n, hipMemcpyHostToDevice, stream);
       sync_done_ = true;
       return;
     }
@@ -87,10 +101,14 @@ public:
       std::lock_guard<std::mutex> g(m_);
       dst_ = static_cast<uint8_t *>(dst);
       src_ = static_cast<const uint8_t *>(src);
+      dev_ = static_cast<uint8_t *>(dev_dst);
+      stream_ = stream;
       n_ = n;
-      // ~4 chunks per thread (the caller joins late), at least 256 KB
+      // ~4 chunks per thread (the caller joins late), at least 256 KB; with
+      // DMA, at least 1 MB so that a transfer is not dominated by its setup
       const size_t parts = 4 * (th_.size() + 1);
-      chunk_ = std::max<size_t>(((n + parts - 1) / parts + 4095) & ~(size_t)4095, (size_t)1 << 18);
+      const size_t minc = dev_dst ? (size_t)1 << 20 : (size_t)1 << 18;
+      chunk_ = std::max<size_t>(((n + parts - 1) / parts + 4095) & ~(size_t)4095, minc);
       nchunks_ = (uint32_t)((n + chunk_ - 1) / chunk_);
       done_ = 0;
       ++gen_;
@@ -99,8 +117,9 @@ public:
     cv_.notify_all();
   }
   // Take part in the copy until no chunk is left, then wait for all of them.
-  void finish() {
-    if (sync_done_) return;
+  // Returns the first failed DMA enqueue (hipSuccess if none).
+  hipError_t finish() {
+    if (sync_done_) return dma_err_;
     uint32_t g;
     {
       std::lock_guard<std::mutex> l(m_);
@@ -110,6 +129,7 @@ public:
     std::unique_lock<std::mutex> lk(m_);
     done_cv_.wait(lk, [this] { return done_ == nchunks_; });
     sync_done_ = true;
+    return dma_err_;
   }
 
 private:
@@ -125,7 +145,10 @@ private:
       const uint32_t i = (uint32_t)t;
       const size_t lo = (size_t)i * chunk_, hi = std::min(n_, lo + chunk_);
       memcpy(dst_ + lo, src_ + lo, hi - lo);
+      hipError_t e = hipSuccess;
+      if (dev_) e = hipMemcpyAsync(dev_ + lo, dst_ + lo, hi - lo, hipMemcpyHostToDevice, stream_);
       std::lock_guard<std::mutex> l(m_);
+      if (e != hipSuccess && dma_err_ == hipSuccess) dma_err_ = e;
       if (++done_ == nchunks_) done_cv_.notify_all();
     }
   }
@@ -149,10 +172,12 @@ private:
   uint64_t gen_ = 0;
   std::atomic<uint64_t> ticket_{0};
   bool stop_ = false, sync_done_ = true;
-  uint8_t *dst_ = nullptr;
+  uint8_t *dst_ = nullptr, *dev_ = nullptr;
   const uint8_t *src_ = nullptr;
+  hipStream_t stream_ = nullptr;
   size_t n_ = 0, chunk_ = 0;
   uint32_t nchunks_ = 0, done_ = 0;
+  hipError_t dma_err_ = hipSuccess;
 };
 
 // Host phases of decode_core (LDT_OPT_HOST_TIMING; read with ldt_host_times).
@@ -177,7 +202,7 @@ struct ldt_ctx {
   int resize_waves_pct = 100;
   int copy_threads = -1; // -1: default (min(4, cores - 1))
   bool host_timing = false;
-  DevBuf d_data, d_plan, d_dstuf, d_coef, d_dcv, d_planes, d_raw, d_dscnt;
+  DevBuf d_data, d_plan, d_dstuf, d_coef, d_brec, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt;
   DevBuf d_perm; // DistributedSampler scratch: 3 int32 arrays of dataset_len
   std::unique_ptr<CopyPool> copier; // host -> pinned copies (created on first use)
   static constexpr int kSlots = 2;
@@ -191,9 +216,9 @@ struct ldt_ctx {
   hipEvent_t done_ev = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_last = false;
-  // the coefficient buffer must be all zero between batches (k_idct restores
-  // it); set while Huffman output may be in it without a k_idct launched
-  // after it, so the next call clears it
+  // the progressive coefficient buffer must be all zero between batches
+  // (k_idct restores it); set while k_prog output may be in it without a
+  // k_idct launched after it, so the next call clears it
   bool coef_dirty = false;
   std::unordered_map<std::string, int> hmap;
   std::vector<HuffTab> htabs;
@@ -329,10 +354,14 @@ CopyPool &copier(ldt_ctx *c) {
   if (!c->copier) {
     int nt = c->copy_threads;
     if (nt < 0) {
-      const unsigned hw = std::thread::hardware_concurrency();
-      nt = (int)std::min(4u, hw > 1 ? hw - 1 : 0u);
+      // the CPUs this process may run on (hardware_concurrency counts the
+      // whole host); ~7 copying threads with the caller saturate PCIe
+      cpu_set_t cs;
+      int cpus = (int)std::thread::hardware_concurrency();
+      if (sched_getaffinity(0, sizeof(cs), &cs) == 0) cpus = CPU_COUNT(&cs);
+      nt = std::min(6, std::max(0, cpus - 2));
     }
-    c->copier.reset(new CopyPool(std::max(0, std::min(nt, 31))));
+    c->copier.reset(new CopyPool(std::max(0, std::min(nt, 31)), c->device));
   }
   return *c->copier;
 }
@@ -340,18 +369,19 @@ CopyPool &copier(ldt_ctx *c) {
 void pinned_copy(ldt_ctx *c, void *dst, const void *src, size_t n) {
   CopyPool &p = copier(c);
   p.start(dst, src, n);
-  p.finish();
+  (void)p.finish();
 }
 
 // Joins an asynchronous cell copy on every exit path of decode_core: the
 // caller's host buffer is borrowed only for the duration of the call.
 struct CopyJoin {
   CopyPool *p = nullptr;
-  void wait() {
-    if (p) p->finish();
+  hipError_t wait() {
+    hipError_t e = p ? p->finish() : hipSuccess;
     p = nullptr;
+    return e;
   }
-  ~CopyJoin() { wait(); }
+  ~CopyJoin() { (void)wait(); }
 };
 
 int ensure_pin(ldt_ctx *c, PinBuf &b, size_t need) {
@@ -471,22 +501,29 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   const uint8_t *cells_host = data_host + base; // cell i at cells_host + (offsets[i] - base)
   if (c->coef_dirty) {
     // an earlier call failed between the Huffman and IDCT launches
-    if (c->d_coef.p) HIPCHK(c, hipMemsetAsync(c->d_coef.p, 0, c->d_coef.cap, s));
+    if (c->d_pcoef.p) HIPCHK(c, hipMemsetAsync(c->d_pcoef.p, 0, c->d_pcoef.cap, s));
     c->coef_dirty = false;
   }
 
-  // ---- pinned slot, then the cells' copy into it on the pool threads: the
-  // header walk below overlaps it (the copy is joined before the H2D) ----
+  // ---- pinned slot, then the cells' way to HBM, which the header walk below
+  // overlaps: the pool threads copy them into the slot in chunks and enqueue
+  // each chunk's H2D DMA as soon as it is copied (a registered range is
+  // DMAed from the caller's pages at once). The copy is joined before the
+  // plan upload and the kernels are enqueued behind it on `s`. ----
   if ((rc = acquire_slot(c))) return rc;
   const int sl = c->slot;
   std::shared_ptr<HostRange> reg; // registered range the H2D reads from
   CopyJoin cj;
+  prof_begin(c, LDT_STAGE_H2D, s);
   if (!data_dev && total_bytes > 0) {
+    if ((rc = ensure_dev(c, c->d_data, (size_t)total_bytes + 16, s))) return rc;
     reg = host_acquire(cells_host, (size_t)total_bytes, c->device);
-    if (!reg) {
+    if (reg) {
+      HIPCHK(c, hipMemcpyAsync(c->d_data.p, cells_host, (size_t)total_bytes, hipMemcpyHostToDevice, s));
+    } else {
       if ((rc = ensure_pin_slots(c, c->h_data, sl, (size_t)total_bytes + 16))) return rc;
       CopyPool &pool = copier(c);
-      pool.start(c->h_data[sl].p, cells_host, (size_t)total_bytes);
+      pool.start(c->h_data[sl].p, cells_host, (size_t)total_bytes, c->d_data.p, s);
       cj.p = &pool;
     }
   }
@@ -506,7 +543,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   std::vector<int> batch_htab_ids; // ctx table id -> index in this batch
   std::unordered_map<int, int> hid_to_batch;
   std::vector<HuffTab> batch_htabs;
-  int64_t dst_total = 0, coef_blocks = 0, plane_total = 0, max_blocks = 0;
+  int64_t dst_total = 0, coef_blocks = 0, pcoef_blocks = 0, plane_total = 0, max_blocks = 0;
   const bool parallel = c->huff_mode != 1;
   const int SB = c->subseq_bits;
   std::vector<int32_t> par_img; // images on the parallel decoder (one workgroup each)
@@ -771,10 +808,15 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     d.dst_off = dst_total;
     dst_total += destuff_region_bytes(d.src_len, d.nseg);
     } // !progressive
-    // each image's coefficients: eight group planes of npad blocks (coef_piece)
+    // each image's coefficients: room for 8 packed units per block (baseline),
+    // and for progressive images also eight dense group planes of npad blocks
+    // (coef_piece) in the progressive buffer (ldt_kernels.hpp)
     d.coef_off = coef_blocks;
     const int64_t nblk = nmcu * d.bpm;
-    coef_blocks += (nblk + kCoefAlign - 1) & ~(int64_t)(kCoefAlign - 1);
+    const int64_t npad = (nblk + kCoefAlign - 1) & ~(int64_t)(kCoefAlign - 1);
+    coef_blocks += npad;
+    d.pcoef_off = pcoef_blocks;
+    if (H.progressive) pcoef_blocks += npad;
     if (nblk > max_blocks) max_blocks = nblk;
     if (resize_fast420(d)) ++n_fast420;
     if (H.width > max_w) max_w = H.width;
@@ -850,24 +892,21 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   // slack: a decoder finishing its last block may read a few hundred bytes
   // past an image's region
   if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 1024, s))) return rc;
-  // coefficients: all zero between batches (k_idct clears every block it
-  // reads), so they are zeroed only when allocated
-  if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 128 + 64, s, true))) return rc;
+  // packed coefficients and block records: written before they are read in
+  // every batch; the progressive planes: all zero between batches (k_idct
+  // clears what it reads), so they are zeroed only when allocated
+  if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 128 + 256, s))) return rc;
+  if ((rc = ensure_dev(c, c->d_brec, (size_t)coef_blocks * 8 + 64, s))) return rc;
+  if (pcoef_blocks > 0 && (rc = ensure_dev(c, c->d_pcoef, (size_t)pcoef_blocks * 128 + 64, s, true))) return rc;
   if ((rc = ensure_dev(c, c->d_dcv, (size_t)coef_blocks * 2 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dscnt, 16 * (size_t)(n_chunks + 1), s))) return rc;
   ht.mark(kHpPlan); // plan blob written, buffers sized
-  prof_begin(c, LDT_STAGE_H2D, s);
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
-    if ((rc = ensure_dev(c, c->d_data, (size_t)total_bytes + 16, s))) return rc;
-    if (total_bytes > 0) {
-      // registered: DMA straight from the caller's pages; else from the slot
-      cj.wait();
-      HIPCHK(c, hipMemcpyAsync(c->d_data.p, reg ? (const void *)cells_host : c->h_data[sl].p,
-                               (size_t)total_bytes, hipMemcpyHostToDevice, s));
-      host_release(reg);
-    }
+    // every chunk copied into the slot and its DMA enqueued
+    HIPCHK(c, cj.wait());
+    host_release(reg);
     dev_cells = static_cast<const uint8_t *>(c->d_data.p);
   }
   HIPCHK(c, hipMemcpyAsync(c->d_plan.p, hp, (size_t)plan_bytes, hipMemcpyHostToDevice, s));
@@ -917,6 +956,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.data = dev_cells;
   w.dstuf = static_cast<uint8_t *>(c->d_dstuf.p);
   w.coef = static_cast<int16_t *>(c->d_coef.p);
+  w.brec = static_cast<uint2 *>(c->d_brec.p);
+  w.pcoef = static_cast<int16_t *>(c->d_pcoef.p);
   w.dcv = static_cast<int16_t *>(c->d_dcv.p);
   w.planes = static_cast<uint8_t *>(c->d_planes.p);
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
@@ -924,7 +965,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
 
   HIPCHK(c, launch_destuff(p, w, s));
   prof_mark(c, LDT_STAGE_DESTUFF, s);
-  c->coef_dirty = true; // until k_idct is enqueued behind the Huffman output
+  c->coef_dirty = p.n_prog > 0; // until k_idct is enqueued behind k_prog's output
   HIPCHK(c, launch_huff_parallel(p, w, s));
   HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_prog(p, w, s));
@@ -1010,7 +1051,7 @@ void ldt_destroy(ldt_ctx *c) {
   if (!c) return;
   DeviceGuard g(c->device);
   (void)hipDeviceSynchronize();
-  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_dcv,
+  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_brec, &c->d_pcoef, &c->d_dcv,
                     &c->d_planes, &c->d_raw, &c->d_dscnt};
   for (DevBuf *b : dbs)
     if (b->p) (void)hipFree(b->p);

@@ -322,11 +322,12 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
 }
 
 // Coefficients of a block are stored in zigzag (decode) order, int16 slots
-// 1..63 (DC lives in dcv); k_idct de-zigzags while dequantising. Slots are
-// combined 8 at a time (16 bytes) in registers and written with one store per
-// touched group instead of one 2-byte scatter per coefficient: a block's
-// coefficient indices only grow, so a group is complete once the decode
-// moves to another group or block.
+// 1..63 (the DC difference goes into the block record; k_idct de-zigzags while
+// dequantising). Slots are combined 8 at a time (a 16-byte group) in
+// registers: a block's coefficient indices only grow, so a group is complete
+// once the decode moves to another group or block. Only nonzero groups are
+// stored, packed (ldt_kernels.hpp): one 16-byte unit each, consecutive for the
+// run's consecutive blocks.
 __device__ __forceinline__ void store_group(uint4 *__restrict__ p, uint64_t lo, uint64_t hi) {
   *p = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
@@ -336,49 +337,67 @@ __device__ __forceinline__ void store_group(uint4 *__restrict__ p, uint64_t lo, 
 // reader's position with cursor -1; a block it enters mid-way (k != 0) is
 // decoded without stores (the previous range writes it), and the run goes on
 // past `stop` until its last block is complete (k back to 0), so every block
-// is written by one lane and no group is shared between lanes. Blocks are
-// base + cursor of the image for cursor in [0, lim) (lim: the segment's
-// blocks not started before the range); the run ends before a block beyond
-// lim. Every value goes into the buffered group at its zigzag slot: the DC
-// difference into slot 0 (the DC predictor scan reads it from group plane 0
-// and writes the absolute DC to dcv; k_idct takes the DC from dcv), nonzero
-// AC coefficients into slots 1..63 of the image's group planes (block
-// base + cursor of coef_img, see coef_piece), which are all zero beforehand
-// (k_idct clears every block it reads). A zero value (EOB, ZRL, a zero DC
-// difference) changes nothing. The loop's one store site flushes the buffered
-// group when a nonzero value opens another (block, group) key; the partial
-// block a run enters has negative keys and is never stored.
+// is written by one lane. Blocks are base + cursor of the image for cursor in
+// [0, lim) (lim: the segment's blocks not started before the range); the run
+// ends before a block beyond lim. Its nonzero groups are packed from unit
+// 8 * base of the image's coefficient region (at most 8 per block, so a run
+// never reaches the next run's units), and each block's record {first unit,
+// group mask | DC difference << 16} is stored when the next block starts (or
+// the run ends). The loop has one group store site: the buffered group is
+// flushed when a nonzero AC value opens another group or a block starts.
 template <class W>
 __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
                                           int &cursor, int lim, uint4 *__restrict__ coef_img,
-                                          int base, int npad) {
-  uint64_t lo = 0, hi = 0; // buffered group: slots 0-3, 4-7
-  int ckey = -1;           // its (cursor << 3) | group; < 0: none
+                                          uint2 *__restrict__ brec_img, int base) {
+  uint64_t lo = 0, hi = 0;           // buffered group: slots 0-3, 4-7
+  int cg = -1;                       // its group index; < 0: none
+  uint32_t wu = (uint32_t)base * 8u; // next unit to store
+  uint32_t bu = wu;                  // first unit of the current block
+  uint32_t gmask = 0;                // groups of the current block stored
+  uint32_t dcd = 0;                  // its DC difference (16 bits)
   bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   while (go) {
-    cursor += st.k == 0 ? 1 : 0;
+    const bool first = st.k == 0; // a block starts: its DC symbol
     const uint32_t pk = R.peek();
     const uint32_t e = lookup(dec, st, pk);
     const int v = ext_value(pk, e);
     const int adv = (int)(e >> 9);
     // a corrupt stream can run k past 63 (a run or ZRL from k > 48): jdhuff.c
     // then stores into natural[k >= 64] = position 63; so does this clamp.
-    // A DC symbol (k = 0, advance 1) lands in slot 0.
     const int slot = min(st.k + adv - 1, 63);
-    const int gkey = (cursor << 3) | (slot >> 3); // cursor -1: negative
-    const bool open = v != 0 && gkey != ckey;
-    if (open && ckey >= 0) store_group(coef_img + coef_piece(base + (ckey >> 3), ckey & 7, npad), lo, hi);
-    lo = open ? 0ull : lo;
-    hi = open ? 0ull : hi;
-    ckey = open ? gkey : ckey;
-    const uint64_t x = (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3));
+    const int g = slot >> 3;
+    const bool opens = !first && v != 0 && g != cg && cursor >= 0;
+    if (cg >= 0 && (first || opens)) {
+      store_group(coef_img + wu, lo, hi);
+      gmask |= 1u << cg;
+      ++wu;
+    }
+    if (first) {
+      if (cursor >= 0) brec_img[base + cursor] = make_uint2(bu, gmask | (dcd << 16));
+      ++cursor;
+      bu = wu;
+      gmask = 0;
+      dcd = (uint32_t)v & 0xFFFFu;
+      cg = -1;
+    }
+    lo = (first || opens) ? 0ull : lo;
+    hi = (first || opens) ? 0ull : hi;
+    cg = opens ? g : cg;
+    // cg < 0: the partial block the run entered (not owned) or a DC symbol
+    const uint64_t x = cg >= 0 ? (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3)) : 0ull;
     lo |= (slot & 4) ? 0ull : x;
     hi |= (slot & 4) ? x : 0ull;
     R.consume((int)(e & 31));
     advance(st, dec, adv);
     go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   }
-  if (ckey >= 0) store_group(coef_img + coef_piece(base + (ckey >> 3), ckey & 7, npad), lo, hi);
+  if (cursor >= 0) {
+    if (cg >= 0) {
+      store_group(coef_img + wu, lo, hi);
+      gmask |= 1u << cg;
+    }
+    brec_img[base + cursor] = make_uint2(bu, gmask | (dcd << 16));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -389,7 +408,7 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
                                                     const HuffTab *__restrict__ htabs,
                                                     const uint8_t *__restrict__ dstuf,
                                                     int16_t *__restrict__ coef,
-                                                    int16_t *__restrict__ dcv,
+                                                    uint2 *__restrict__ brec,
                                                     int32_t *__restrict__ status) {
   const int img = blockIdx.x;
   // nseg 0: progressive (k_prog); sub_bits > 0: the parallel decoder
@@ -411,7 +430,7 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
     const int blk0 = sg.mcu_first * d.bpm; // image-relative
     // a valid segment ends inside its bits; 64 bits of slack bound a corrupt one
     write_run(R, st, dec, pbias + seg_bits + 64, cursor, total, reinterpret_cast<uint4 *>(coef + d.coef_off * 64),
-              blk0, coef_npad(d));
+              brec + d.coef_off, blk0);
     if (R.p - pbias > seg_bits || cursor + 1 < total || st.k != 0) status[img] = 3; // truncated
   }
 }
@@ -420,7 +439,7 @@ hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s)
   if (p.n_serial == 0) return hipSuccess;
   const size_t tab_lds = (size_t)huff_tab_lds(p.max_tabs);
   hipLaunchKernelGGL(k_huff_serial, dim3(p.n), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,
-                     w.dstuf, w.coef, w.dcv, w.status);
+                     w.dstuf, w.coef, w.brec, w.status);
   return hipGetLastError();
 }
 
@@ -428,11 +447,11 @@ hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s)
 // DC predictors (jdhuff.c: last_dc_val[ci] += diff, reset to 0 at every
 // restart marker, process_restart) of one image, by its NT-thread workgroup:
 // thread t owns a run of consecutive blocks; a segmented scan over the threads
-// carries the per-component sums. The DC differences are read from slot 0 of
-// group plane 0 (write_run), the absolute DC (JCOEF, truncated) is stored in
-// v. `scr` is 4*NT/64 ints of LDS; contains __syncthreads.
+// carries the per-component sums. The DC differences are read from the block
+// records (write_run), the absolute DC (JCOEF, truncated) is stored in v.
+// `scr` is 4*NT/64 ints of LDS; contains __syncthreads.
 template <int NT>
-__device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint4 *__restrict__ plane0,
+__device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint2 *__restrict__ rec,
                                               int16_t *__restrict__ v, LDS_AS int32_t *scr) {
   static_assert(NT % 64 == 0, "whole waves");
   const int tid = threadIdx.x;
@@ -459,7 +478,7 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint4 *__r
         flag = 1;
       }
       const int c = (int)((compmap >> (2 * b)) & 3);
-      const int dv = *reinterpret_cast<const int16_t *>(plane0 + x);
+      const int dv = (int)(int16_t)(rec[x].y >> 16);
       s0 += c == 0 ? dv : 0;
       s1 += c == 1 ? dv : 0;
       s2 += c == 2 ? dv : 0;
@@ -511,7 +530,7 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint4 *__r
   for (int64_t x = lo; x < hi; ++x) {
     if (sp == 0) r0 = r1 = r2 = 0;
     const int c = (int)((compmap >> (2 * b)) & 3);
-    const int dv = *reinterpret_cast<const int16_t *>(plane0 + x);
+    const int dv = (int)(int16_t)(rec[x].y >> 16);
     r0 += c == 0 ? dv : 0;
     r1 += c == 1 ? dv : 0;
     r2 += c == 2 ? dv : 0;
@@ -524,20 +543,20 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint4 *__r
 // k_dc_scan: the DC predictors of the serial decoder's images (the parallel
 // decoder's workgroups scan their own image after the write pass).
 __global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ descs,
-                                                 const int16_t *__restrict__ coef,
+                                                 const uint2 *__restrict__ brec,
                                                  int16_t *__restrict__ dcv,
                                                  const int32_t *__restrict__ status) {
   __shared__ int32_t scr[4 * 256 / 64];
   const int img = blockIdx.x;
   // progressive: dcv holds the final DC; sub_bits > 0: k_huff_image
   if (status[img] != 0 || descs[img].nseg == 0 || descs[img].sub_bits > 0) return;
-  dc_scan_image<256>(descs[img], reinterpret_cast<const uint4 *>(coef + descs[img].coef_off * 64),
-                     dcv + descs[img].coef_off, (LDS_AS int32_t *)scr);
+  dc_scan_image<256>(descs[img], brec + descs[img].coef_off, dcv + descs[img].coef_off,
+                     (LDS_AS int32_t *)scr);
 }
 
 hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_serial == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dc_scan, dim3(p.n), dim3(256), 0, s, p.descs, w.coef, w.dcv, w.status);
+  hipLaunchKernelGGL(k_dc_scan, dim3(p.n), dim3(256), 0, s, p.descs, w.brec, w.dcv, w.status);
   return hipGetLastError();
 }
 
@@ -737,6 +756,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
                                              const Segment *__restrict__ segs, const Dec &dec,
                                              int warm, uint64_t t_setup, ImgLds &sh,
                                              int16_t *__restrict__ coef,
+                                             uint2 *__restrict__ brec,
                                              int16_t *__restrict__ dcv,
                                              int32_t *__restrict__ status, int img,
                                              int32_t *__restrict__ dbg) {
@@ -928,7 +948,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     R.src = src;
     R.seek(g.pbias + wp);
     write_run(R, st, dec, wstop, cursor, total - bstart, reinterpret_cast<uint4 *>(coef + d.coef_off * 64),
-              base, coef_npad(d));
+              brec + d.coef_off, base);
     if (g.j == sg.sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;
@@ -952,8 +972,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   // ---- DC predictors (the serial path runs k_dc_scan instead) ----
   if (!trunc) {
     __syncthreads(); // sh is free from here: its first 256 bytes are the scan scratch
-    dc_scan_image<kHuffThreads>(d, reinterpret_cast<const uint4 *>(coef + d.coef_off * 64), dcv + d.coef_off,
-                                (LDS_AS int32_t *)&sh);
+    dc_scan_image<kHuffThreads>(d, brec + d.coef_off, dcv + d.coef_off, (LDS_AS int32_t *)&sh);
   }
 }
 
@@ -961,8 +980,8 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
     const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
-    int16_t *__restrict__ coef, int16_t *__restrict__ dcv, int32_t *__restrict__ status,
-    int32_t *__restrict__ dbg) {
+    int16_t *__restrict__ coef, uint2 *__restrict__ brec, int16_t *__restrict__ dcv,
+    int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
   __shared__ ImgLds sh;
   const int img = par_img[blockIdx.x];
   if (status[img] != 0) return;
@@ -1037,11 +1056,11 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   if (dbg && tid == 0) atomicAdd(dbg + 8, (int)(t_setup - t_start));
   const int warm = (d.sub_bits * warm_pct) / 100;
   if (in_lds)
-    image_decode(LdsWords{(lds_cu32)dyn_lds}, d, segs, dec, warm, t_setup, sh, coef, dcv, status,
+    image_decode(LdsWords{(lds_cu32)dyn_lds}, d, segs, dec, warm, t_setup, sh, coef, brec, dcv, status,
                  img, dbg);
   else
     image_decode(GlobWords{reinterpret_cast<const uint32_t *>(base)}, d, segs, dec, warm, t_setup,
-                 sh, coef, dcv, status, img, dbg);
+                 sh, coef, brec, dcv, status, img, dbg);
 }
 
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {
@@ -1052,7 +1071,7 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
   if (attr != hipSuccess) return attr;
   const size_t lds = (size_t)p.win_bytes + huff_tab_lds(p.max_tabs);
   hipLaunchKernelGGL(k_huff_image, dim3(p.n_par), dim3(kHuffThreads), lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.dcv,
+                     p.htabs, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.brec, w.dcv,
                      w.status, p.redo);
   return hipGetLastError();
 }

@@ -438,15 +438,16 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
 // One lane per 8x8 block: the whole block stays in registers for both
 // passes (no transposes, no barriers between them). A workgroup covers
 // kIdctBlocksPerWg consecutive blocks of one image; each lane loads its
-// block's eight 16-B groups straight into registers (no LDS tile: occupancy is
-// set by registers alone, so more blocks are in flight). The group-plane
-// layout (coef_piece) makes each group load a contiguous 1 KB per wave.
+// block's 16-B groups straight into registers (no LDS tile: occupancy is set
+// by registers alone, so more blocks are in flight).
 //
-// Coefficient buffer contract (with the Huffman decoders and k_prog): all
-// zero between batches. The Huffman pass writes only nonzero AC coefficient
-// groups; this kernel reads every block (also of images whose decode failed)
-// and writes zeros back over the groups that are not zero, so the buffer
-// needs no memset per batch (it is cleared once when allocated).
+// Baseline images: the block record gives the block's nonzero groups (mask)
+// and where their packed units start (ldt_kernels.hpp); only those are read,
+// the others are zero, and nothing is written back. Progressive images: the
+// dense group planes of `pcoef` (one contiguous 1 KB per group and wave), and
+// zeros are written back over the groups that were not zero — the all-zero
+// contract of that buffer with k_prog (also for failed images), so it needs no
+// memset per batch.
 constexpr int kIdctBlocksPerWg = 256; // = threads
 // jpeg_natural_order: zigzag position -> natural (row-major) index
 constexpr int kZigzagNat[64] = {
@@ -456,7 +457,9 @@ constexpr int kZigzagNat[64] = {
 
 __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__restrict__ descs,
                                               const uint16_t *__restrict__ qtabs,
-                                              int16_t *__restrict__ coef,
+                                              const int16_t *__restrict__ coef,
+                                              const uint2 *__restrict__ brec,
+                                              int16_t *__restrict__ pcoef,
                                               const int16_t *__restrict__ dcv,
                                               uint8_t *__restrict__ planes,
                                               const int32_t *__restrict__ status) {
@@ -468,6 +471,8 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
   if (b0 >= nblk) return;
   const int tid = threadIdx.x;
   const bool ok = status[img] == 0;
+  const bool prog = d.nseg == 0;
+  if (!ok && !prog) return; // packed coefficients need no clearing
   const int nb = (int)min((int64_t)kIdctBlocksPerWg, nblk - b0);
   // quant tables in zigzag order, like the coefficients
   for (int i = tid; i < 64 * d.ncomp; i += kIdctBlocksPerWg)
@@ -475,20 +480,26 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
   __syncthreads();
   if (tid >= nb) return;
   const int64_t blk = b0 + tid;
-  // the lane's block straight into registers (one 128-B line per lane), and
-  // zeros back over the groups that held coefficients (the all-zero
-  // invariant; a failed image's blocks are cleared too)
-  // Group planes (coef_piece): group r of the wave's 64 consecutive blocks is
-  // one contiguous 1 KB, so each of the 8 loads and zero stores is coalesced.
-  uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
-  const int npad = coef_npad(d);
   uint4 raw[8];
+  if (prog) {
+    uint4 *cimg = reinterpret_cast<uint4 *>(pcoef + d.pcoef_off * 64);
+    const int npad = coef_npad(d);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) raw[r] = cimg[coef_piece((int)blk, r, npad)];
+    for (int r = 0; r < 8; ++r) raw[r] = cimg[coef_piece((int)blk, r, npad)];
 #pragma unroll
-  for (int r = 0; r < 8; ++r)
-    if ((raw[r].x | raw[r].y | raw[r].z | raw[r].w) != 0) cimg[coef_piece((int)blk, r, npad)] = make_uint4(0u, 0u, 0u, 0u);
-  if (!ok) return;
+    for (int r = 0; r < 8; ++r)
+      if ((raw[r].x | raw[r].y | raw[r].z | raw[r].w) != 0) cimg[coef_piece((int)blk, r, npad)] = make_uint4(0u, 0u, 0u, 0u);
+    if (!ok) return;
+  } else {
+    // record, then the nonzero groups from consecutive units
+    const uint2 rc = brec[d.coef_off + blk];
+    const uint4 *u = reinterpret_cast<const uint4 *>(coef + d.coef_off * 64) + rc.x;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      raw[r] = make_uint4(0u, 0u, 0u, 0u);
+      if ((rc.y >> r) & 1u) raw[r] = *u++;
+    }
+  }
   const int64_t m = blk / d.bpm;
   const int b = (int)(blk - m * d.bpm);
   const int comp = d.bcomp[b];
@@ -866,7 +877,7 @@ hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n == 0 || p.max_blocks == 0) return hipSuccess;
   dim3 grid((unsigned)((p.max_blocks + kIdctBlocksPerWg - 1) / kIdctBlocksPerWg), (unsigned)p.n);
-  hipLaunchKernelGGL(k_idct, grid, dim3(kIdctBlocksPerWg), 0, s, p.descs, p.qtabs, w.coef, w.dcv, w.planes,
+  hipLaunchKernelGGL(k_idct, grid, dim3(kIdctBlocksPerWg), 0, s, p.descs, p.qtabs, w.coef, w.brec, w.pcoef, w.dcv, w.planes,
                      w.status);
   return hipGetLastError();
 }

@@ -50,18 +50,28 @@ struct DevPlan {
   const int32_t *chunk_img; // chunk -> image
 };
 
-// Coefficient buffer layout, per image: eight group planes. Zigzag slots
-// 8g..8g+7 of image-relative block ib (a 16-byte piece) sit at piece
-// g * npad + ib of the image's region (npad = its block count rounded up to
-// 64; regions start at coef_off * 64 int16s, coef_off % 64 == 0). The 64 lanes
-// of a wave that own 64 consecutive blocks then read or clear group g of all
-// of them with one contiguous 1 KB access (k_idct), while the Huffman write
-// pass still stores whole 16-byte groups at one multiply-add per address.
+// Coefficients of baseline images (the Huffman decoders' output), packed:
+// a block's nonzero 16-byte groups (zigzag slots 8g..8g+7, slot 0 unused) in
+// increasing g, one 16-byte unit each, in the image's region of `coef`
+// (starting at coef_off * 64 int16s, room for 8 units per block). The lane
+// that owns a run of consecutive blocks writes their units contiguously from
+// unit 8 * (its first block), so every 64-byte segment of the region is
+// filled by one lane's consecutive stores. Block ib's record brec[coef_off +
+// ib] = {first unit (image-relative), nonzero-group mask | DC difference << 16}.
+// Nothing is read that was not written in the same batch, so the buffer needs
+// no clearing.
+//
+// Progressive images (k_prog) refine coefficients over many scans, so they
+// keep dense per-image group planes in `pcoef`: zigzag slots 8g..8g+7 of block
+// ib at piece g * npad + ib of the region at pcoef_off * 64 int16s (npad = the
+// block count rounded up to 64), so the 64 lanes of a wave owning 64
+// consecutive blocks read group g with one contiguous 1 KB access. That buffer
+// is all zero between batches (k_idct clears the groups it read).
 constexpr int kCoefAlign = 64;
 __host__ __device__ __forceinline__ int coef_npad(const ImgDesc &d) {
   return (int)(((int64_t)d.mcux * d.mcuy * d.bpm + kCoefAlign - 1) & ~(int64_t)(kCoefAlign - 1));
 }
-// Index of the 16-byte piece (block ib, group g) from the image's region start.
+// Index of the 16-byte piece (block ib, group g) from the image's dense region.
 // npad < 2^24 (LDT_MAX_DIM 8192, 4:4:4), so this is one 24-bit multiply-add.
 __host__ __device__ __forceinline__ uint32_t coef_piece(int ib, int g, int npad) {
   return __umul24((unsigned)g, (unsigned)npad) + (unsigned)ib;
@@ -70,10 +80,10 @@ __host__ __device__ __forceinline__ uint32_t coef_piece(int ib, int g, int npad)
 struct DevWork {
   const uint8_t *data;  // compressed cells
   uint8_t *dstuf;       // destuffed entropy data
-  int16_t *coef;        // AC coefficients (the DC slot of each block is unused), in
-                        // group planes (coef_piece); all zero between batches (k_idct
-                        // clears every block it reads)
-  int16_t *dcv;         // per block: DC difference (Huffman), then absolute DC (dc_scan_image)
+  int16_t *coef;        // baseline images: packed nonzero coefficient groups (above)
+  uint2 *brec;          // baseline images: per block {first unit, group mask | DC diff << 16}
+  int16_t *pcoef;       // progressive images: dense group planes, all zero between batches
+  int16_t *dcv;         // per block (coef_off): absolute DC (dc_scan_image; k_prog)
   uint8_t *planes;      // component planes
   int32_t *status;      // per image
   int4 *ds_cnt;         // per destuff chunk: kept bytes, RSTn markers, end marker seen

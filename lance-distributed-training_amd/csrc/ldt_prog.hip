@@ -2,9 +2,10 @@
 //
 // jdphuff.c restated (decode_mcu_DC_first / DC_refine / AC_first / AC_refine,
 // EOB runs, restart intervals) with jdcoefct.c's full-image coefficient
-// buffer: every scan updates the image's blocks in the same coefficient
-// buffer the baseline decoder fills (zigzag slots 1..63 in `coef`, the final
-// DC value in `dcv`), so k_idct and the resize kernels then run unchanged.
+// buffer: every scan updates the image's blocks in dense group planes
+// (zigzag slots 1..63 in `pcoef`, the final DC value in `dcv`), which k_idct
+// reads (and clears) instead of the baseline decoders' packed groups; the
+// resize kernels run unchanged.
 //
 // Four 64-lane workgroups per progressive image, one per independent scan
 // chain (DC scans; each component's AC scans). A scan's Huffman decode is a
@@ -227,7 +228,7 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
                                              const ProgScan *__restrict__ scans,
                                              const ProgTab *__restrict__ ptabs,
                                              const uint8_t *__restrict__ data,
-                                             int16_t *__restrict__ coef,
+                                             int16_t *__restrict__ pcoef,
                                              int16_t *__restrict__ dcv,
                                              const int32_t *__restrict__ status) {
   __shared__ ProgLds Lw[kWaves];
@@ -350,7 +351,7 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
           uint64_t nz = 0;
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const int4 v = reinterpret_cast<const int4 *>(coef + d.coef_off * 64)[coef_piece((int)blk, q, coef_npad(d))];
+            const int4 v = reinterpret_cast<const int4 *>(pcoef + d.pcoef_off * 64)[coef_piece((int)blk, q, coef_npad(d))];
             dst[q] = v;
             const uint32_t w[4] = {(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w};
 #pragma unroll
@@ -471,7 +472,7 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
           const int4 *src = reinterpret_cast<const int4 *>(L.blk[lane]);
 #pragma unroll
           for (int q = 0; q < 8; ++q)
-            reinterpret_cast<int4 *>(coef + d.coef_off * 64)[coef_piece((int)(gb - d.coef_off), q, coef_npad(d))] = src[q];
+            reinterpret_cast<int4 *>(pcoef + d.pcoef_off * 64)[coef_piece((int)(gb - d.coef_off), q, coef_npad(d))] = src[q];
         }
       }
       if (piped) { // publish chunk ci once the wave's stores are done
@@ -494,7 +495,7 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
 hipError_t launch_prog(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_prog == 0) return hipSuccess;
   hipLaunchKernelGGL(k_prog, dim3(4 * p.n_prog), dim3(64 * kWaves), 0, s, p.descs, p.prog_img, p.pscans, p.ptabs,
-                     w.data, w.coef, w.dcv, w.status);
+                     w.data, w.pcoef, w.dcv, w.status);
   return hipGetLastError();
 }
 

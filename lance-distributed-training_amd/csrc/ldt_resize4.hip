@@ -493,6 +493,9 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
           f.y = lc[min((uint32_t)acc[i][1] >> kPrecisionBits, 255u)];
           f.z = lc[min((uint32_t)acc[i][2] >> kPrecisionBits, 255u)];
           f.w = lc[min((uint32_t)acc[i][3] >> kPrecisionBits, 255u)];
+#ifdef LDT_EXP_NOSTORE
+          if (f.x + f.y + f.z + f.w == 12345.f)
+#endif
           *reinterpret_cast<float4 *>(out + (((int64_t)img * 3 + vc[i]) * kOut + oy0 + j) * kOut + vo[i]) = f;
         }
       }
@@ -509,9 +512,15 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   fetch(pa, ya0);
   for (int y = ya0; y < yb; y += 2) {
     stage(pa, y);
+#ifdef LDT_EXP_STORE_FIRST
+    wave_lds_fence();
+    vertical(y);
+    if (y + 2 < yb) fetch(pa, y + 2);
+#else
     if (y + 2 < yb) fetch(pa, y + 2);
     wave_lds_fence();
     vertical(y);
+#endif
     horizontal(y);
     wave_lds_fence();
   }

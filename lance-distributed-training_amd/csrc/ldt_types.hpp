@@ -44,6 +44,9 @@ struct ImgDesc {
   // progressive (SOF2) images: scans [prog_first, prog_first + prog_count) of
   // the plan's scan table, decoded by k_prog; nseg == 0 (no baseline segments)
   int32_t prog_first, prog_count;
+  // progressive images: first block of the image's dense group planes in the
+  // progressive coefficient buffer (DevWork::pcoef)
+  int64_t pcoef_off;
 };
 
 // k_resize4's fast staging path: 4:2:0 YCbCr with both chroma planes

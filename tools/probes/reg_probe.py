@@ -5,7 +5,6 @@ import os
 import sys
 import time
 
-os.environ["LDT_HOST_TIMING"] = "1"
 R = os.path.join(os.path.dirname(__file__), "..", "..")
 sys.path.insert(0, R)
 sys.path.insert(0, os.path.join(R, "lance-distributed-training_amd"))
@@ -26,8 +25,13 @@ for k in range(2):
                                          names=["image", "label"]))
 
 
-def run(tag):
+from ldt_amd import _lib  # noqa: E402
+
+
+def run(tag, threads=-1):
     pipe = ldt_amd.DecodePipeline(depth=3, device=dev)
+    pipe.set_option(_lib.OPT_HOST_TIMING, 1)
+    pipe.set_option(_lib.OPT_COPY_THREADS, threads)
     for i in range(6):
         pipe.decode(bs[i % 2])
     torch.cuda.synchronize()
@@ -40,11 +44,15 @@ def run(tag):
     torch.cuda.synchronize()
     tot = (time.perf_counter() - t0) * 1e3 / 60
     pipe.check()
-    print(f"{tag}: ms/step {tot:.3f}  host ms/call median {np.median(calls):.3f} max {max(calls):.3f}",
-          flush=True)
+    us, n = pipe.host_times(reset=True)
+    # the first 6 warm-up calls are included in the host phase sums
+    print(f"{tag}: ms/step {tot:.3f}  host ms/call median {np.median(calls):.3f} max {max(calls):.3f}  "
+          f"phases us/call " + " ".join(f"{k}={v / max(n, 1):.1f}" for k, v in us.items()), flush=True)
 
 
 run("copy")
+for t in (0, 2, 8, 12):
+    run(f"copy threads={t}", t)
 for b in bs:
     ldt_amd.register_host(b.column(0), device=dev)
 run("registered")
