@@ -14,6 +14,10 @@ Three legs of the same workload, each timed between barriers (max over ranks):
                     driver contract); everything else of the path is timed;
   value_host_input  the plug-in boundary: host pa.RecordBatches through the
                     pipelined to_tensor_fn (pinned copy + H2D every step);
+  config_legs       BASELINE configs[2] and [3] as written, in a c2 run: the
+                    dataset leg below over FOOD101-shaped cells with
+                    ShardedBatchSampler (c3) and ImageNet-shaped cells with
+                    ShardedFragmentSampler(pad=True) (c4), batch 128 per rank;
   value_dataset     the reference's iterable loop: an Arrow/Lance dataset of the
                     workload's cells read through LanceDataset + the sampler
                     (ShardedBatchSampler; ShardedFragmentSampler(pad=True) with
@@ -205,6 +209,8 @@ def main():
                     help="epochs in the dataset leg's timed region (each re-plans, as a training loop does)")
     ap.add_argument("--resize-impl", type=int, default=0,
                     help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize420 for 4:2:0; 1 k_resize4)")
+    ap.add_argument("--no-config-legs", action="store_true",
+                    help="skip the configs[2]/configs[3] dataset legs (c3, c4) of a c2 run")
     ap.add_argument("--registered", action="store_true",
                     help="also time the host leg with the cell buffers page-locked in place (ldt_register_host)")
     args = ap.parse_args()
@@ -345,6 +351,26 @@ def main():
     if args.workload != "c5" and args.dataset_batches > 0:
         value_dataset, dataset_info = dataset_rate(args, wl, B, world, rank, dev, cells_all, labels_all,
                                                    barrier, max_over_ranks)
+    # BASELINE configs[2] (c3) and configs[3] (c4) as written — the reference's
+    # iterable loop over FOOD101-shaped / ImageNet-shaped cells with its own
+    # sampler — in the same run as the headline, so that every N of a scaling
+    # sweep reports them beside it (the headline stays c2, whose per-N values
+    # the sweep's efficiency is computed from)
+    config_legs = {}
+    if args.workload == "c2" and args.dataset_batches > 0 and not args.no_config_legs:
+        for cw in ("c3", "c4"):
+            cwl = WORKLOADS[cw]
+            cb = cwl["batch"]
+            cc, cl = [], []
+            for k in range(2):
+                c_, l_ = make_cells(cw, cb, seed=7000 + 1000 * rank + k)
+                cc += c_
+                cl += list(l_)
+            v, info = dataset_rate(args, cwl, cb, world, rank, dev, cc, cl, barrier, max_over_ranks, tag=cw)
+            config_legs[cw] = {"workload": f"{cw}: {cwl['desc']}", "value": round(v, 1),
+                               "value_per_gpu": round(v / world, 1), "per_gpu_batch": cb,
+                               "compressed_bytes_per_img": round(float(np.mean([len(c) for c in cc])), 1),
+                               "dataset_leg": info}
 
     # standalone launch durations (one batch in flight, after the timed region)
     standalone = None
@@ -414,6 +440,8 @@ def main():
         res["host_us_per_call"] = host_us
     if value_registered is not None:
         res["value_host_registered"] = round(value_registered, 1)
+    if config_legs:
+        res["config_legs"] = config_legs
     if value_dataset is not None:
         res["value_dataset"] = round(value_dataset, 1)
         res["value_dataset_per_gpu"] = round(value_dataset / world, 1)
@@ -461,7 +489,7 @@ def main():
         dist.destroy_process_group()
 
 
-def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over_ranks):
+def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over_ranks, tag=None):
     """The reference's iterable loop (lance_iterable.py:53-72, :86-116) over an
     Arrow/Lance dataset of this workload's cells: LanceDataset + the sampler +
     the pipelined to_tensor_fn, `dataset_epochs` full epochs per rank in the
@@ -495,7 +523,8 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     rows = sum(sizes)
     import tempfile
 
-    path = os.path.join(tempfile.gettempdir(), f"ldt_bench_ds_{os.environ.get('MASTER_PORT', '0')}_{args.workload}_{world}")
+    path = os.path.join(tempfile.gettempdir(),
+                        f"ldt_bench_ds_{os.environ.get('MASTER_PORT', '0')}_{tag or args.workload}_{world}")
     if rank == 0:
         n = len(cells)
         idx = np.arange(rows) % n

@@ -161,6 +161,18 @@ int ldt_unregister_host(ldt_ctx *ctx, const void *ptr);
  * into per_image_status[n] (for LDT_OPT_SYNC_STATUS = 0). */
 int ldt_fetch_status(ldt_ctx *ctx, void *stream, int32_t *per_image_status, int64_t n);
 
+/* Tickets (LDT_OPT_SYNC_STATUS = 0): every decode call that enqueues work gets
+ * the next ticket of its context (1, 2, ...; ldt_last_ticket returns the most
+ * recent one, 0 before any). A context holds the device-side status of its
+ * last two calls: ldt_fetch_status_ticket waits only for that call's batch
+ * (not for newer work on the stream) and merges its errors as above; a ticket
+ * older than the last two returns LDT_ERR_ARG. This lets a pipeline check a
+ * batch two uses of the context later, long after it completed, instead of
+ * synchronising on the batch just before it. Replaces the per-batch status
+ * check of lance_iterable.py:42 (PIL raising in the loop) without a stall. */
+int64_t ldt_last_ticket(ldt_ctx *ctx);
+int ldt_fetch_status_ticket(ldt_ctx *ctx, int64_t ticket, int32_t *per_image_status, int64_t n);
+
 /* Profiling (LDT_OPT_PROFILE = 1): waits for every recorded stage event and
  * adds the elapsed milliseconds of each stage since the last reset into
  * ms_out[stage] and the number of timed launches into count_out[stage]

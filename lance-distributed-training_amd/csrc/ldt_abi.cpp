@@ -202,7 +202,7 @@ struct ldt_ctx {
   int resize_waves_pct = 100;
   int copy_threads = -1; // -1: default (min(4, cores - 1))
   bool host_timing = false;
-  DevBuf d_data, d_plan, d_dstuf, d_coef, d_brec, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt;
+  DevBuf d_data, d_plan, d_dstuf, d_coef, d_brec, d_bcarry, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt;
   DevBuf d_perm; // DistributedSampler scratch: 3 int32 arrays of dataset_len
   std::unique_ptr<CopyPool> copier; // host -> pinned copies (created on first use)
   static constexpr int kSlots = 2;
@@ -210,8 +210,17 @@ struct ldt_ctx {
   hipEvent_t slot_ev[kSlots] = {nullptr, nullptr};
   bool slot_used[kSlots] = {false, false};
   int slot = 0;
-  int32_t *h_status = nullptr; // pinned
-  size_t h_status_cap = 0;
+  // per-image status of the last decode on each pinned slot (device part,
+  // copied back at the end of the batch): ticket = the call's number, event
+  // = recorded after the copy, so a status can be read `kSlots` calls later
+  // without waiting for the newer batches (ldt_fetch_status_ticket)
+  int32_t *h_status[kSlots] = {nullptr, nullptr}; // pinned
+  size_t h_status_cap[kSlots] = {0, 0};
+  hipEvent_t st_ev[kSlots] = {nullptr, nullptr};
+  int64_t st_ticket[kSlots] = {-1, -1};
+  int64_t st_n[kSlots] = {0, 0};
+  int64_t tickets = 0; // decode calls that enqueued work
+  int last_sl = 0;     // slot of the most recent decode
   int64_t last_n = 0;
   hipEvent_t done_ev = nullptr;
   hipStream_t last_stream = nullptr;
@@ -896,7 +905,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   // every batch; the progressive planes: all zero between batches (k_idct
   // clears what it reads), so they are zeroed only when allocated
   if ((rc = ensure_dev(c, c->d_coef, (size_t)coef_blocks * 128 + 256, s))) return rc;
-  if ((rc = ensure_dev(c, c->d_brec, (size_t)coef_blocks * 8 + 64, s))) return rc;
+  if ((rc = ensure_dev(c, c->d_brec, (size_t)coef_blocks * 4 + 64, s))) return rc;
+  if ((rc = ensure_dev(c, c->d_bcarry, (size_t)coef_blocks / 16 + 64, s))) return rc;
   if (pcoef_blocks > 0 && (rc = ensure_dev(c, c->d_pcoef, (size_t)pcoef_blocks * 128 + 64, s, true))) return rc;
   if ((rc = ensure_dev(c, c->d_dcv, (size_t)coef_blocks * 2 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
@@ -956,7 +966,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.data = dev_cells;
   w.dstuf = static_cast<uint8_t *>(c->d_dstuf.p);
   w.coef = static_cast<int16_t *>(c->d_coef.p);
-  w.brec = static_cast<uint2 *>(c->d_brec.p);
+  w.brec = static_cast<uint32_t *>(c->d_brec.p);
+  w.bcarry = static_cast<uint32_t *>(c->d_bcarry.p);
   w.pcoef = static_cast<int16_t *>(c->d_pcoef.p);
   w.dcv = static_cast<int16_t *>(c->d_dcv.p);
   w.planes = static_cast<uint8_t *>(c->d_planes.p);
@@ -987,15 +998,24 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   c->cur_ev = nullptr;
 
   ht.mark(kHpLaunch); // kernels launched
-  // ---- per-image status back to the host ----
-  if ((size_t)n > c->h_status_cap) {
-    if (c->h_status) HIPCHK(c, hipHostFree(c->h_status));
-    c->h_status = nullptr;
-    if (hipHostMalloc((void **)&c->h_status, 4 * (size_t)n, hipHostMallocDefault) != hipSuccess)
+  // ---- per-image status back to the host, into this slot's buffer ----
+  if ((size_t)n > c->h_status_cap[sl]) {
+    if (c->h_status[sl]) {
+      HIPCHK(c, hipEventSynchronize(c->st_ev[sl])); // its last copy has landed
+      HIPCHK(c, hipHostFree(c->h_status[sl]));
+    }
+    c->h_status[sl] = nullptr;
+    c->h_status_cap[sl] = 0;
+    c->st_ticket[sl] = -1;
+    if (hipHostMalloc((void **)&c->h_status[sl], 4 * (size_t)n, hipHostMallocDefault) != hipSuccess)
       return set_err(c, LDT_ERR_NOMEM, "hipHostMalloc(status) failed");
-    c->h_status_cap = (size_t)n;
+    c->h_status_cap[sl] = (size_t)n;
   }
-  HIPCHK(c, hipMemcpyAsync(c->h_status, w.status, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(c->h_status[sl], w.status, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipEventRecord(c->st_ev[sl], s));
+  c->st_ticket[sl] = ++c->tickets;
+  c->st_n[sl] = n;
+  c->last_sl = sl;
   c->last_n = n;
   if ((rc = finish_call(c, s))) return rc;
   ht.mark(kHpStatus); // status copy enqueued
@@ -1004,7 +1024,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     HIPCHK(c, hipStreamSynchronize(s));
     bool bad = false;
     for (int64_t i = 0; i < n; ++i) {
-      if (status_out[i] == 0) status_out[i] = c->h_status[i];
+      if (status_out[i] == 0) status_out[i] = c->h_status[sl][i];
       if (status_out[i]) bad = true;
     }
     if (bad) return set_err(c, LDT_ERR_IMAGE, "one or more images failed to decode");
@@ -1031,7 +1051,8 @@ ldt_ctx *ldt_create(int device, size_t max_batch_bytes, int max_n) {
   c->device = device;
   DeviceGuard g(device);
   for (int k = 0; k < ldt_ctx::kSlots; ++k)
-    if (hipEventCreateWithFlags(&c->slot_ev[k], hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&c->slot_ev[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->st_ev[k], hipEventDisableTiming) != hipSuccess) {
       delete c;
       return nullptr;
     }
@@ -1051,7 +1072,7 @@ void ldt_destroy(ldt_ctx *c) {
   if (!c) return;
   DeviceGuard g(c->device);
   (void)hipDeviceSynchronize();
-  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_brec, &c->d_pcoef, &c->d_dcv,
+  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_brec, &c->d_bcarry, &c->d_pcoef, &c->d_dcv,
                     &c->d_planes, &c->d_raw, &c->d_dscnt};
   for (DevBuf *b : dbs)
     if (b->p) (void)hipFree(b->p);
@@ -1059,8 +1080,9 @@ void ldt_destroy(ldt_ctx *c) {
     if (c->h_data[k].p) (void)hipHostFree(c->h_data[k].p);
     if (c->h_plan[k].p) (void)hipHostFree(c->h_plan[k].p);
     if (c->slot_ev[k]) (void)hipEventDestroy(c->slot_ev[k]);
+    if (c->st_ev[k]) (void)hipEventDestroy(c->st_ev[k]);
+    if (c->h_status[k]) (void)hipHostFree(c->h_status[k]);
   }
-  if (c->h_status) (void)hipHostFree(c->h_status);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   delete c;
 }
@@ -1226,17 +1248,38 @@ int ldt_stage_times(ldt_ctx *c, double *ms_out, int64_t *count_out, int reset) {
   return LDT_OK;
 }
 
+namespace {
+int merge_status(ldt_ctx *c, int sl, int32_t *st, int64_t n) {
+  if (n > c->st_n[sl]) return set_err(c, LDT_ERR_ARG, "n exceeds that batch");
+  bool bad = false;
+  for (int64_t i = 0; i < n; ++i) {
+    if (st[i] == 0) st[i] = c->h_status[sl][i];
+    if (st[i]) bad = true;
+  }
+  return bad ? set_err(c, LDT_ERR_IMAGE, "one or more images failed to decode") : LDT_OK;
+}
+} // namespace
+
 int ldt_fetch_status(ldt_ctx *c, void *stream, int32_t *st, int64_t n) {
   if (!c || !st) return LDT_ERR_ARG;
   DeviceGuard g(c->device);
   HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-  if (n > c->last_n) return set_err(c, LDT_ERR_ARG, "n exceeds last batch");
-  bool bad = false;
-  for (int64_t i = 0; i < n; ++i) {
-    if (st[i] == 0) st[i] = c->h_status[i];
-    if (st[i]) bad = true;
-  }
-  return bad ? set_err(c, LDT_ERR_IMAGE, "one or more images failed to decode") : LDT_OK;
+  if (c->tickets == 0) return n == 0 ? LDT_OK : set_err(c, LDT_ERR_ARG, "no decode yet");
+  return merge_status(c, c->last_sl, st, n);
+}
+
+int64_t ldt_last_ticket(ldt_ctx *c) { return c ? c->tickets : -1; }
+
+int ldt_fetch_status_ticket(ldt_ctx *c, int64_t ticket, int32_t *st, int64_t n) {
+  if (!c || !st) return LDT_ERR_ARG;
+  DeviceGuard g(c->device);
+  for (int k = 0; k < ldt_ctx::kSlots; ++k)
+    if (c->st_ticket[k] == ticket && ticket > 0) {
+      HIPCHK(c, hipEventSynchronize(c->st_ev[k]));
+      return merge_status(c, k, st, n);
+    }
+  return set_err(c, LDT_ERR_ARG, "status of call %lld is no longer held (last %lld)", (long long)ticket,
+                 (long long)c->tickets);
 }
 
 int ldt_resize_raw(ldt_ctx *c, const uint8_t *hwc, int hwc_is_device, int64_t n, int h, int w,

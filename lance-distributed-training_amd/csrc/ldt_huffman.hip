@@ -8,8 +8,9 @@
 // Bits past a segment's end read as zero (jdhuff.c inserts zeros at a marker;
 // here k_destuff leaves kSegPad zero bytes after every segment).
 // Input: destuffed segments (k_destuff). Output: int16 coefficients in zigzag
-// order, image-relative block (mcu, b) = mcu * bpm + b in the image's group
-// planes (coef_piece; raw, dequantised in k_idct).
+// order, image-relative block (mcu, b) = mcu * bpm + b, as packed nonzero
+// 16-byte groups plus a 4-byte record per block (ldt_kernels.hpp; raw,
+// dequantised in k_idct), and the absolute DC values in the records.
 //
 // The symbol step is uniform for DC and AC: a table entry carries the bits to
 // consume (code + magnitude), the magnitude width s and the advance of the
@@ -327,10 +328,45 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
 // registers: a block's coefficient indices only grow, so a group is complete
 // once the decode moves to another group or block. Only nonzero groups are
 // stored, packed (ldt_kernels.hpp): one 16-byte unit each, consecutive for the
-// run's consecutive blocks.
-__device__ __forceinline__ void store_group(uint4 *__restrict__ p, uint64_t lo, uint64_t hi) {
-  *p = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+// run's consecutive blocks, and four units (one 64-byte segment) leave
+// together, so that a segment reaches the L2 as one burst from one lane.
+__device__ __forceinline__ void store_units(uint4 *__restrict__ p, const uint4 &a, const uint4 &b,
+                                            const uint4 &c, const uint4 &d) {
+  p[0] = a;
+  p[1] = b;
+  p[2] = c;
+  p[3] = d;
 }
+
+// q0 <- q1 <- q2 <- q3 <- x when p (the unit queue of write_run).
+__device__ __forceinline__ uint32_t sel(bool p, uint32_t a, uint32_t b) { return p ? a : b; }
+__device__ __forceinline__ void shift_in(bool p, uint4 &q0, uint4 &q1, uint4 &q2, uint4 &q3, const uint4 &x) {
+  q0.x = sel(p, q1.x, q0.x); q0.y = sel(p, q1.y, q0.y); q0.z = sel(p, q1.z, q0.z); q0.w = sel(p, q1.w, q0.w);
+  q1.x = sel(p, q2.x, q1.x); q1.y = sel(p, q2.y, q1.y); q1.z = sel(p, q2.z, q1.z); q1.w = sel(p, q2.w, q1.w);
+  q2.x = sel(p, q3.x, q2.x); q2.y = sel(p, q3.y, q2.y); q2.z = sel(p, q3.z, q2.z); q2.w = sel(p, q3.w, q2.w);
+  q3.x = sel(p, x.x, q3.x); q3.y = sel(p, x.y, q3.y); q3.z = sel(p, x.z, q3.z); q3.w = sel(p, x.w, q3.w);
+}
+
+// Where a run's block records and chunk carries go: the workgroup's LDS
+// (k_huff_image, copied out coalesced after the DC scan) or global memory.
+// put_if: the LDS sink stores unconditionally (to a scratch word when `p` is
+// false), which keeps the write loop free of branches around it.
+struct RecLds {
+  LDS_AS uint32_t *rec, *carry, *scratch;
+  __device__ __forceinline__ void put(int ib, uint32_t v) const { rec[ib] = v; }
+  __device__ __forceinline__ void put_if(bool p, int ib, uint32_t v) const { *(p ? rec + ib : scratch) = v; }
+  __device__ __forceinline__ void carry_if(bool p, int c, uint32_t u) const { *(p ? carry + c : scratch) = u; }
+};
+struct RecGlob {
+  uint32_t *rec, *carry;
+  __device__ __forceinline__ void put(int ib, uint32_t v) const { rec[ib] = v; }
+  __device__ __forceinline__ void put_if(bool p, int ib, uint32_t v) const {
+    if (p) rec[ib] = v;
+  }
+  __device__ __forceinline__ void carry_if(bool p, int c, uint32_t u) const {
+    if (p) carry[c] = u;
+  }
+};
 
 // Coefficient-writing decode of one range, with block ownership: a block
 // belongs to the range that decodes its DC symbol. The run starts at the
@@ -341,21 +377,26 @@ __device__ __forceinline__ void store_group(uint4 *__restrict__ p, uint64_t lo, 
 // [0, lim) (lim: the segment's blocks not started before the range); the run
 // ends before a block beyond lim. Its nonzero groups are packed from unit
 // 8 * base of the image's coefficient region (at most 8 per block, so a run
-// never reaches the next run's units), and each block's record {first unit,
-// group mask | DC difference << 16} is stored when the next block starts (or
-// the run ends). The loop has one group store site: the buffered group is
-// flushed when a nonzero AC value opens another group or a block starts.
-template <class W>
+// never reaches the next run's units; 8 * base is segment-aligned). Each
+// block's record (gmask | run start << 8 | DC difference << 16, see
+// ldt_kernels.hpp) is stored when the next block starts or the run ends, and
+// a block at a multiple of 64 publishes its first unit as its chunk's carry.
+// The loop has one group site: the buffered group joins the unit queue when a
+// nonzero AC value opens another group or a block starts.
+template <class W, class RS>
 __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
                                           int &cursor, int lim, uint4 *__restrict__ coef_img,
-                                          uint2 *__restrict__ brec_img, int base) {
+                                          const RS &rs, int base) {
   uint64_t lo = 0, hi = 0;           // buffered group: slots 0-3, 4-7
   int cg = -1;                       // its group index; < 0: none
-  uint32_t wu = (uint32_t)base * 8u; // next unit to store
-  uint32_t bu = wu;                  // first unit of the current block
-  uint32_t gmask = 0;                // groups of the current block stored
+  uint4 q0 = make_uint4(0u, 0u, 0u, 0u), q1 = q0, q2 = q0, q3 = q0; // the segment's units (q3 newest)
+  uint32_t wu = (uint32_t)base * 8u; // units stored or queued
+  uint32_t gmask = 0;                // groups of the current block
   uint32_t dcd = 0;                  // its DC difference (16 bits)
   bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
+  // Branch-free bookkeeping (selects, predicated LDS stores): a wave's lanes
+  // take the group and block paths at different symbols, so branches around
+  // them would be executed by the whole wave at almost every symbol anyway.
   while (go) {
     const bool first = st.k == 0; // a block starts: its DC symbol
     const uint32_t pk = R.peek();
@@ -367,22 +408,49 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     const int slot = min(st.k + adv - 1, 63);
     const int g = slot >> 3;
     const bool opens = !first && v != 0 && g != cg && cursor >= 0;
-    if (cg >= 0 && (first || opens)) {
-      store_group(coef_img + wu, lo, hi);
+    const bool flush = cg >= 0 && (first || opens);
+    // component-wise selects (a select of whole uint4 values becomes a
+    // select of their addresses in scratch memory)
+    const uint4 cur = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+#if defined(LDT_EXP_WR_NOQ)
+    if (flush) {
+      coef_img[wu] = cur;
       gmask |= 1u << cg;
       ++wu;
     }
-    if (first) {
-      if (cursor >= 0) brec_img[base + cursor] = make_uint2(bu, gmask | (dcd << 16));
-      ++cursor;
-      bu = wu;
-      gmask = 0;
-      dcd = (uint32_t)v & 0xFFFFu;
-      cg = -1;
+#elif defined(LDT_EXP_WR_QBRANCH)
+    if (flush) {
+      q0 = q1;
+      q1 = q2;
+      q2 = q3;
+      q3 = cur;
+      gmask |= 1u << cg;
+      ++wu;
+      if ((wu & 3u) == 0) store_units(coef_img + (wu - 4), q0, q1, q2, q3);
     }
+#else
+    shift_in(flush, q0, q1, q2, q3, cur);
+    gmask |= flush ? 1u << (cg & 7) : 0u;
+    wu += flush ? 1u : 0u;
+    if (flush && (wu & 3u) == 0) store_units(coef_img + (wu - 4), q0, q1, q2, q3);
+#endif
+    // a block starts: the previous one's record, then this block's state
+#ifdef LDT_EXP_WR_RBRANCH
+    if (first) {
+      if (cursor >= 0) rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
+      ++cursor;
+      if (((base + cursor) & 63) == 0) rs.carry_if(true, (base + cursor) >> 6, wu);
+    }
+#else
+    rs.put_if(first && cursor >= 0, base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
+    cursor += first ? 1 : 0;
+    rs.carry_if(first && ((base + cursor) & 63) == 0, (base + cursor) >> 6, wu);
+#endif
+    gmask = first ? 0u : gmask;
+    dcd = first ? (uint32_t)v & 0xFFFFu : dcd;
     lo = (first || opens) ? 0ull : lo;
     hi = (first || opens) ? 0ull : hi;
-    cg = opens ? g : cg;
+    cg = first ? -1 : (opens ? g : cg);
     // cg < 0: the partial block the run entered (not owned) or a DC symbol
     const uint64_t x = cg >= 0 ? (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3)) : 0ull;
     lo |= (slot & 4) ? 0ull : x;
@@ -392,11 +460,37 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   }
   if (cursor >= 0) {
+    bool last = false; // the buffered group of the last block joined the queue
     if (cg >= 0) {
-      store_group(coef_img + wu, lo, hi);
+      q0 = q1;
+      q1 = q2;
+      q2 = q3;
+      q3 = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
       gmask |= 1u << cg;
+      ++wu;
+      last = true;
     }
-    brec_img[base + cursor] = make_uint2(bu, gmask | (dcd << 16));
+    rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
+#ifdef LDT_EXP_WR_NOQ
+    if (last) coef_img[wu - 1] = q3;
+    return;
+#endif
+    // the queued units not stored yet: the newest (wu & 3) of q0..q3, or all
+    // four when that last group completed a segment
+    const uint32_t k = wu & 3u;
+    uint4 *p = coef_img + (wu - k);
+    if (k == 0 && last) {
+      store_units(coef_img + (wu - 4), q0, q1, q2, q3);
+    } else if (k == 3) {
+      p[0] = q1;
+      p[1] = q2;
+      p[2] = q3;
+    } else if (k == 2) {
+      p[0] = q2;
+      p[1] = q3;
+    } else if (k == 1) {
+      p[0] = q3;
+    }
   }
 }
 
@@ -408,7 +502,8 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
                                                     const HuffTab *__restrict__ htabs,
                                                     const uint8_t *__restrict__ dstuf,
                                                     int16_t *__restrict__ coef,
-                                                    uint2 *__restrict__ brec,
+                                                    uint32_t *__restrict__ brec,
+                                                    uint32_t *__restrict__ bcarry,
                                                     int32_t *__restrict__ status) {
   const int img = blockIdx.x;
   // nseg 0: progressive (k_prog); sub_bits > 0: the parallel decoder
@@ -430,7 +525,7 @@ __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ 
     const int blk0 = sg.mcu_first * d.bpm; // image-relative
     // a valid segment ends inside its bits; 64 bits of slack bound a corrupt one
     write_run(R, st, dec, pbias + seg_bits + 64, cursor, total, reinterpret_cast<uint4 *>(coef + d.coef_off * 64),
-              brec + d.coef_off, blk0);
+              RecGlob{brec + d.coef_off, bcarry + d.coef_off / 64}, blk0);
     if (R.p - pbias > seg_bits || cursor + 1 < total || st.k != 0) status[img] = 3; // truncated
   }
 }
@@ -439,7 +534,7 @@ hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s)
   if (p.n_serial == 0) return hipSuccess;
   const size_t tab_lds = (size_t)huff_tab_lds(p.max_tabs);
   hipLaunchKernelGGL(k_huff_serial, dim3(p.n), dim3(64), tab_lds, s, p.descs, p.segs, p.htabs,
-                     w.dstuf, w.coef, w.brec, w.status);
+                     w.dstuf, w.coef, w.brec, w.bcarry, w.status);
   return hipGetLastError();
 }
 
@@ -448,11 +543,12 @@ hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s)
 // restart marker, process_restart) of one image, by its NT-thread workgroup:
 // thread t owns a run of consecutive blocks; a segmented scan over the threads
 // carries the per-component sums. The DC differences are read from the block
-// records (write_run), the absolute DC (JCOEF, truncated) is stored in v.
-// `scr` is 4*NT/64 ints of LDS; contains __syncthreads.
-template <int NT>
-__device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint2 *__restrict__ rec,
-                                              int16_t *__restrict__ v, LDS_AS int32_t *scr) {
+// records (bits 16-31, write_run) and replaced there by the absolute DC
+// (JCOEF, truncated) in place: each record is read and written by one thread.
+// REC is the records' pointer type (LDS or global). `scr` is 4*NT/64 ints of
+// LDS; contains __syncthreads.
+template <int NT, class REC>
+__device__ __forceinline__ void dc_scan_image(const ImgDesc &d, REC rec, LDS_AS int32_t *scr) {
   static_assert(NT % 64 == 0, "whole waves");
   const int tid = threadIdx.x;
   const int bpm = d.bpm;
@@ -478,7 +574,7 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint2 *__r
         flag = 1;
       }
       const int c = (int)((compmap >> (2 * b)) & 3);
-      const int dv = (int)(int16_t)(rec[x].y >> 16);
+      const int dv = (int)rec[x] >> 16;
       s0 += c == 0 ? dv : 0;
       s1 += c == 1 ? dv : 0;
       s2 += c == 2 ? dv : 0;
@@ -530,11 +626,13 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint2 *__r
   for (int64_t x = lo; x < hi; ++x) {
     if (sp == 0) r0 = r1 = r2 = 0;
     const int c = (int)((compmap >> (2 * b)) & 3);
-    const int dv = (int)(int16_t)(rec[x].y >> 16);
+    const uint32_t rv = rec[x];
+    const int dv = (int)rv >> 16;
     r0 += c == 0 ? dv : 0;
     r1 += c == 1 ? dv : 0;
     r2 += c == 2 ? dv : 0;
-    v[x] = (int16_t)(c == 0 ? r0 : c == 1 ? r1 : r2);
+    const int dc = c == 0 ? r0 : c == 1 ? r1 : r2;
+    rec[x] = (rv & 0xFFFFu) | ((uint32_t)dc << 16);
     b = b + 1 == bpm ? 0 : b + 1;
     sp = sp + 1 == seglen ? 0 : sp + 1;
   }
@@ -543,20 +641,18 @@ __device__ __forceinline__ void dc_scan_image(const ImgDesc &d, const uint2 *__r
 // k_dc_scan: the DC predictors of the serial decoder's images (the parallel
 // decoder's workgroups scan their own image after the write pass).
 __global__ void __launch_bounds__(256) k_dc_scan(const ImgDesc *__restrict__ descs,
-                                                 const uint2 *__restrict__ brec,
-                                                 int16_t *__restrict__ dcv,
+                                                 uint32_t *__restrict__ brec,
                                                  const int32_t *__restrict__ status) {
   __shared__ int32_t scr[4 * 256 / 64];
   const int img = blockIdx.x;
   // progressive: dcv holds the final DC; sub_bits > 0: k_huff_image
   if (status[img] != 0 || descs[img].nseg == 0 || descs[img].sub_bits > 0) return;
-  dc_scan_image<256>(descs[img], brec + descs[img].coef_off, dcv + descs[img].coef_off,
-                     (LDS_AS int32_t *)scr);
+  dc_scan_image<256>(descs[img], brec + descs[img].coef_off, (LDS_AS int32_t *)scr);
 }
 
 hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_serial == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dc_scan, dim3(p.n), dim3(256), 0, s, p.descs, w.brec, w.dcv, w.status);
+  hipLaunchKernelGGL(k_dc_scan, dim3(p.n), dim3(256), 0, s, p.descs, w.brec, w.status);
   return hipGetLastError();
 }
 
@@ -590,8 +686,10 @@ hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s) {
 //            flows to the right);
 //   prefix   exclusive scan of the block counts: each range's first block;
 //   write    every lane decodes its range again from its true entry and stores
-//            coefficients (zigzag groups) and DC differences;
-//   dc       the workgroup adds the DC predictors (dc_scan_image).
+//            its blocks' nonzero coefficient groups (packed) and their records
+//            (into LDS when the image has <= kRecCap blocks);
+//   dc       the workgroup adds the DC predictors in the records
+//            (dc_scan_image), which then leave in coalesced stores.
 // An image with more than kMaxParSegs restart segments takes k_huff_serial
 // instead: one lane per segment is already parallel there.
 // ===========================================================================
@@ -661,22 +759,35 @@ __device__ __forceinline__ bool count_run(Rd<W> &R, int32_t range_start, int32_t
 // Static LDS of k_huff_image (the window and the tables are dynamic): the
 // decode state of every slot, so that a round's re-decodes can be packed into
 // the first waves of the workgroup (any lane may work on any slot).
+constexpr int kRecCap = 8192; // block records an image keeps in LDS during the write pass
 struct ImgLds {
   int32_t ex_p[kHuffThreads];  // exit position (segment-relative)
-  // entry of the slot's current trajectory and its checkpoint positions,
-  // relative to the range start j*S (< S + 32 <= kMaxParS + 32)
-  uint16_t en_p[kHuffThreads];
-  uint16_t cp_p0[kHuffThreads], cp_p1[kHuffThreads];
-  uint16_t ex_bk[kHuffThreads], en_bk[kHuffThreads]; // (3b << 8) | k
-  uint16_t cp_bk0[kHuffThreads], cp_bk1[kHuffThreads];
-  uint16_t cp_a0[kHuffThreads], cp_a1[kHuffThreads]; // blocks counted up to the checkpoints
-  uint16_t nblk[kHuffThreads]; // blocks started in the range (S <= kMaxParS bounds it)
-  uint16_t work[kHuffThreads]; // this round's slots to re-decode
-  // the slot's previous trajectory (memo): entry, exit (relative to the range
-  // start) and block count; m_en_bk = 0xFFFF: none
-  uint16_t m_en_p[kHuffThreads], m_en_bk[kHuffThreads];
-  uint16_t m_ex_p[kHuffThreads], m_ex_bk[kHuffThreads], m_nblk[kHuffThreads];
-  uint8_t cp_n[kHuffThreads];
+  union {
+    // decode state of the slots (phase 1 and the rounds)
+    struct {
+      // entry of the slot's current trajectory and its checkpoint positions,
+      // relative to the range start j*S (< S + 32 <= kMaxParS + 32)
+      uint16_t en_p[kHuffThreads];
+      uint16_t cp_p0[kHuffThreads], cp_p1[kHuffThreads];
+      uint16_t ex_bk[kHuffThreads], en_bk[kHuffThreads]; // (3b << 8) | k
+      uint16_t cp_bk0[kHuffThreads], cp_bk1[kHuffThreads];
+      uint16_t cp_a0[kHuffThreads], cp_a1[kHuffThreads]; // blocks counted up to the checkpoints
+      uint16_t nblk[kHuffThreads]; // blocks started in the range (S <= kMaxParS bounds it)
+      uint16_t work[kHuffThreads]; // this round's slots to re-decode
+      // the slot's previous trajectory (memo): entry, exit (relative to the
+      // range start) and block count; m_en_bk = 0xFFFF: none
+      uint16_t m_en_p[kHuffThreads], m_en_bk[kHuffThreads];
+      uint16_t m_ex_p[kHuffThreads], m_ex_bk[kHuffThreads], m_nblk[kHuffThreads];
+      uint8_t cp_n[kHuffThreads];
+    };
+    // write pass (images of <= kRecCap blocks): the block records and chunk
+    // carries (ldt_kernels.hpp), copied out coalesced after the DC scan
+    struct {
+      uint32_t rec[kRecCap];
+      uint32_t carry[kRecCap / 64];
+      uint32_t rec_scratch; // target of the write loop's predicated-off stores
+    };
+  };
   int32_t seg_first[kMaxParSegs + 1]; // sub_first of the image's segments; [nseg] = slots
   int32_t seg_pb[kMaxParSegs];        // segment start: bit position in the window
   int32_t seg_nb[kMaxParSegs];        // segment length in bits
@@ -756,8 +867,8 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
                                              const Segment *__restrict__ segs, const Dec &dec,
                                              int warm, uint64_t t_setup, ImgLds &sh,
                                              int16_t *__restrict__ coef,
-                                             uint2 *__restrict__ brec,
-                                             int16_t *__restrict__ dcv,
+                                             uint32_t *__restrict__ brec,
+                                             uint32_t *__restrict__ bcarry,
                                              int32_t *__restrict__ status, int img,
                                              int32_t *__restrict__ dbg) {
   const int tid = threadIdx.x;
@@ -935,6 +1046,9 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   const uint64_t t_scan = wall_clock64();
 
   // ---- write pass from the true entry ----
+  // block records into LDS (the slot state is dead from here) when they fit
+  const int64_t nblk_img = (int64_t)d.mcux * d.mcuy * d.bpm;
+  const bool rec_lds = nblk_img <= kRecCap;
   bool trunc = false;
   if (live) {
     // blocks of the segment started before this range: the first block whose
@@ -947,15 +1061,21 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     Rd<W> R;
     R.src = src;
     R.seek(g.pbias + wp);
-    write_run(R, st, dec, wstop, cursor, total - bstart, reinterpret_cast<uint4 *>(coef + d.coef_off * 64),
-              brec + d.coef_off, base);
+    uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
+    if (rec_lds)
+      write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
+                RecLds{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry, (LDS_AS uint32_t *)&sh.rec_scratch},
+                base);
+    else
+      write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
+                RecGlob{brec + d.coef_off, bcarry + d.coef_off / 64}, base);
     if (g.j == sg.sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;
     }
   }
-  // the image's DC differences are complete. The barrier's workgroup-scope
-  // fence publishes them to the other waves (one CU, one vector L1); an
+  // the image's records are complete. The barrier's workgroup-scope fence
+  // publishes them to the other waves (one CU, one vector L1 and the LDS); an
   // agent-scope fence would write back and invalidate the XCD's whole L2.
   trunc = __syncthreads_or(trunc);
   // diagnostic phase times (10 ns ticks summed over images; ldt_debug_counters)
@@ -969,10 +1089,19 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     atomicAdd(dbg + 14, sh.need_waves);
     atomicAdd(dbg + 4, sh.memo_hits);
   }
-  // ---- DC predictors (the serial path runs k_dc_scan instead) ----
-  if (!trunc) {
-    __syncthreads(); // sh is free from here: its first 256 bytes are the scan scratch
-    dc_scan_image<kHuffThreads>(d, brec + d.coef_off, dcv + d.coef_off, (LDS_AS int32_t *)&sh);
+  if (trunc) return; // a failed image's records are never read
+  // ---- DC predictors (the serial path runs k_dc_scan instead), in the
+  // records; then the LDS records and carries leave in coalesced stores ----
+  // (sh's first 256 bytes, ex_p, are the scan scratch)
+  if (rec_lds) {
+    dc_scan_image<kHuffThreads>(d, (LDS_AS uint32_t *)sh.rec, (LDS_AS int32_t *)&sh);
+    __syncthreads();
+    uint32_t *gr = brec + d.coef_off;
+    for (int ib = tid; ib < (int)nblk_img; ib += kHuffThreads) gr[ib] = sh.rec[ib];
+    uint32_t *gc = bcarry + d.coef_off / 64;
+    for (int c = tid; c < (int)((nblk_img + 63) >> 6); c += kHuffThreads) gc[c] = sh.carry[c];
+  } else {
+    dc_scan_image<kHuffThreads>(d, brec + d.coef_off, (LDS_AS int32_t *)&sh);
   }
 }
 
@@ -980,7 +1109,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
     const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
-    int16_t *__restrict__ coef, uint2 *__restrict__ brec, int16_t *__restrict__ dcv,
+    int16_t *__restrict__ coef, uint32_t *__restrict__ brec, uint32_t *__restrict__ bcarry,
     int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
   __shared__ ImgLds sh;
   const int img = par_img[blockIdx.x];
@@ -1056,11 +1185,11 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   if (dbg && tid == 0) atomicAdd(dbg + 8, (int)(t_setup - t_start));
   const int warm = (d.sub_bits * warm_pct) / 100;
   if (in_lds)
-    image_decode(LdsWords{(lds_cu32)dyn_lds}, d, segs, dec, warm, t_setup, sh, coef, brec, dcv, status,
-                 img, dbg);
+    image_decode(LdsWords{(lds_cu32)dyn_lds}, d, segs, dec, warm, t_setup, sh, coef, brec, bcarry,
+                 status, img, dbg);
   else
     image_decode(GlobWords{reinterpret_cast<const uint32_t *>(base)}, d, segs, dec, warm, t_setup,
-                 sh, coef, brec, dcv, status, img, dbg);
+                 sh, coef, brec, bcarry, status, img, dbg);
 }
 
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {
@@ -1071,7 +1200,7 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
   if (attr != hipSuccess) return attr;
   const size_t lds = (size_t)p.win_bytes + huff_tab_lds(p.max_tabs);
   hipLaunchKernelGGL(k_huff_image, dim3(p.n_par), dim3(kHuffThreads), lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.brec, w.dcv,
+                     p.htabs, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.brec, w.bcarry,
                      w.status, p.redo);
   return hipGetLastError();
 }

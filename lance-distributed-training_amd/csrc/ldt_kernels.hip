@@ -458,7 +458,8 @@ constexpr int kZigzagNat[64] = {
 __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__restrict__ descs,
                                               const uint16_t *__restrict__ qtabs,
                                               const int16_t *__restrict__ coef,
-                                              const uint2 *__restrict__ brec,
+                                              const uint32_t *__restrict__ brec,
+                                              const uint32_t *__restrict__ bcarry,
                                               int16_t *__restrict__ pcoef,
                                               const int16_t *__restrict__ dcv,
                                               uint8_t *__restrict__ planes,
@@ -477,11 +478,12 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
   // quant tables in zigzag order, like the coefficients
   for (int i = tid; i < 64 * d.ncomp; i += kIdctBlocksPerWg)
     s_q[i >> 6][i & 63] = qtabs[d.qt[i >> 6] * 64 + kZigzagNat[i & 63]];
-  __syncthreads();
-  if (tid >= nb) return;
   const int64_t blk = b0 + tid;
   uint4 raw[8];
+  int32_t dc = 0;
   if (prog) {
+    __syncthreads();
+    if (tid >= nb) return;
     uint4 *cimg = reinterpret_cast<uint4 *>(pcoef + d.pcoef_off * 64);
     const int npad = coef_npad(d);
 #pragma unroll
@@ -490,15 +492,35 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
     for (int r = 0; r < 8; ++r)
       if ((raw[r].x | raw[r].y | raw[r].z | raw[r].w) != 0) cimg[coef_piece((int)blk, r, npad)] = make_uint4(0u, 0u, 0u, 0u);
     if (!ok) return;
+    dc = dcv[d.coef_off + blk];
   } else {
-    // record, then the nonzero groups from consecutive units
-    const uint2 rc = brec[d.coef_off + blk];
-    const uint4 *u = reinterpret_cast<const uint4 *>(coef + d.coef_off * 64) + rc.x;
+    // the block's record; its first unit by a segmented scan over the wave's
+    // 64 consecutive blocks: a run start begins at 8 * blk, every other
+    // block where its predecessor's groups end, and the wave's first block
+    // (unless a run starts there) at its chunk's carry
+    const bool in = tid < nb;
+    const uint32_t rc = in ? brec[d.coef_off + blk] : 0u;
+    const int lane = tid & 63;
+    const uint32_t cnt = (uint32_t)__popc(rc & 255u);
+    int fl = (rc >> 8) & 1;
+    uint32_t v = fl ? 8u * (uint32_t)blk + cnt : cnt; // end of this block's units
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int pf = __shfl_up(fl, off);
+      const uint32_t pv = (uint32_t)__shfl_up((int)v, off);
+      if (lane >= off && !fl) v += pv;
+      fl |= lane >= off ? pf : 0;
+    }
+    const uint32_t carry = fl ? 0u : bcarry[(d.coef_off + (blk & ~(int64_t)63)) >> 6];
+    __syncthreads();
+    if (!in) return;
+    const uint4 *u = reinterpret_cast<const uint4 *>(coef + d.coef_off * 64) + (carry + v - cnt);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       raw[r] = make_uint4(0u, 0u, 0u, 0u);
-      if ((rc.y >> r) & 1u) raw[r] = *u++;
+      if ((rc >> r) & 1u) raw[r] = *u++;
     }
+    dc = (int32_t)rc >> 16;
   }
   const int64_t m = blk / d.bpm;
   const int b = (int)(blk - m * d.bpm);
@@ -519,7 +541,7 @@ __global__ void __launch_bounds__(kIdctBlocksPerWg) k_idct(const ImgDesc *__rest
       ws[kZigzagNat[8 * r + 2 * j + 1]] = __mul24(hi, (int32_t)(qw[j] >> 16));
     }
   }
-  ws[0] = (int32_t)dcv[d.coef_off + blk] * (int32_t)q[0]; // DC: absolute value after the predictor scan
+  ws[0] = dc * (int32_t)q[0]; // DC: absolute value after the predictor scan
   // pass 1: columns (CONST_BITS 13, PASS1_BITS 2). A column whose AC terms are
   // all zero gives DC << 2 exactly (jidctint.c shortcut); the butterfly runs
   // when any lane of the wave needs it.
@@ -877,7 +899,7 @@ hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n == 0 || p.max_blocks == 0) return hipSuccess;
   dim3 grid((unsigned)((p.max_blocks + kIdctBlocksPerWg - 1) / kIdctBlocksPerWg), (unsigned)p.n);
-  hipLaunchKernelGGL(k_idct, grid, dim3(kIdctBlocksPerWg), 0, s, p.descs, p.qtabs, w.coef, w.brec, w.pcoef, w.dcv, w.planes,
+  hipLaunchKernelGGL(k_idct, grid, dim3(kIdctBlocksPerWg), 0, s, p.descs, p.qtabs, w.coef, w.brec, w.bcarry, w.pcoef, w.dcv, w.planes,
                      w.status);
   return hipGetLastError();
 }

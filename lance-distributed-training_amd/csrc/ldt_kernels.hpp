@@ -53,11 +53,17 @@ struct DevPlan {
 // Coefficients of baseline images (the Huffman decoders' output), packed:
 // a block's nonzero 16-byte groups (zigzag slots 8g..8g+7, slot 0 unused) in
 // increasing g, one 16-byte unit each, in the image's region of `coef`
-// (starting at coef_off * 64 int16s, room for 8 units per block). The lane
-// that owns a run of consecutive blocks writes their units contiguously from
-// unit 8 * (its first block), so every 64-byte segment of the region is
-// filled by one lane's consecutive stores. Block ib's record brec[coef_off +
-// ib] = {first unit (image-relative), nonzero-group mask | DC difference << 16}.
+// (starting at coef_off * 64 int16s, room for 8 units per block). A run (the
+// blocks one decoder lane owns, consecutive) writes its blocks' units
+// contiguously from unit 8 * (its first block), so its first unit is
+// 64-byte aligned and it writes whole 64-byte segments. Per block a 4-byte
+// record brec[coef_off + ib] = nonzero-group mask (bits 0-7) | run start
+// (bit 8) | DC (bits 16-31: the difference from the decoder, the absolute
+// value after the predictor scan), and per 64 blocks a carry
+// bcarry[coef_off / 64 + c] = the first unit of block 64c. A block's first
+// unit is then 8 * ib at a run start, else its predecessor's first unit plus
+// the predecessor's group count: k_idct, whose waves own 64 consecutive
+// blocks, gets it with one segmented wave scan from the chunk's carry.
 // Nothing is read that was not written in the same batch, so the buffer needs
 // no clearing.
 //
@@ -81,9 +87,10 @@ struct DevWork {
   const uint8_t *data;  // compressed cells
   uint8_t *dstuf;       // destuffed entropy data
   int16_t *coef;        // baseline images: packed nonzero coefficient groups (above)
-  uint2 *brec;          // baseline images: per block {first unit, group mask | DC diff << 16}
+  uint32_t *brec;       // baseline images: per block group mask | run start << 8 | DC << 16
+  uint32_t *bcarry;     // baseline images: per 64 blocks the first unit of the chunk's first block
   int16_t *pcoef;       // progressive images: dense group planes, all zero between batches
-  int16_t *dcv;         // per block (coef_off): absolute DC (dc_scan_image; k_prog)
+  int16_t *dcv;         // progressive images, per block (coef_off): absolute DC (k_prog)
   uint8_t *planes;      // component planes
   int32_t *status;      // per image
   int4 *ds_cnt;         // per destuff chunk: kept bytes, RSTn markers, end marker seen

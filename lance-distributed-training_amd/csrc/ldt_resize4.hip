@@ -179,7 +179,11 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   // kernel is LDS-bound). JPEG rows stay plain: the skew's extra registers
   // cost a wave per SIMD there, which is worth more than its 2-way conflicts.
   constexpr bool kJpeg = SRC == 0 || SRC == 2;
+#ifdef LDT_EXP_JPEG_SKEW
+  constexpr bool kSkew = true;
+#else
   constexpr bool kSkew = !kJpeg;
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
   for (int i = tid; i < 768; i += (int)blockDim.x) s_lut[i] = lut[i];

@@ -54,7 +54,8 @@ HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status")
 EXPORTED = (
     "ldt_create", "ldt_destroy", "ldt_last_error", "ldt_set_option", "ldt_version",
     "ldt_decode_batch", "ldt_decode_batch_large", "ldt_decode_batch_resident",
-    "ldt_register_host", "ldt_unregister_host", "ldt_fetch_status", "ldt_stage_times", "ldt_host_times", "ldt_resize_raw", "ldt_shard_ranges",
+    "ldt_register_host", "ldt_unregister_host", "ldt_fetch_status", "ldt_last_ticket", "ldt_fetch_status_ticket",
+    "ldt_stage_times", "ldt_host_times", "ldt_resize_raw", "ldt_shard_ranges",
     "ldt_shard_fragments", "ldt_distributed_indices",
 )
 
@@ -119,6 +120,9 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_decode_batch_large.argtypes = [vp, vp, vp, i64, i64, vp, vp, i64, vp, vp, vp, vp, vp]
         L.ldt_decode_batch_resident.argtypes = [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
         L.ldt_fetch_status.argtypes = [vp, vp, vp, i64]
+        L.ldt_last_ticket.argtypes = [vp]
+        L.ldt_last_ticket.restype = i64
+        L.ldt_fetch_status_ticket.argtypes = [vp, i64, vp, i64]
         L.ldt_stage_times.argtypes = [vp, vp, vp, i32]
         L.ldt_host_times.argtypes = [vp, vp, vp, i32]
         L.ldt_resize_raw.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, vp, vp]
@@ -132,7 +136,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_unregister_host.argtypes = [vp, vp]
         for name in ("ldt_set_option", "ldt_decode_batch", "ldt_decode_batch_large", "ldt_register_host",
                      "ldt_unregister_host",
-                     "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_resize_raw", "ldt_stage_times", "ldt_host_times",
+                     "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_fetch_status_ticket", "ldt_resize_raw", "ldt_stage_times", "ldt_host_times",
                      "ldt_shard_ranges", "ldt_shard_fragments", "ldt_distributed_indices",
                      "ldt_debug_resample_coeffs",
                      "ldt_debug_counters"):

@@ -49,20 +49,35 @@ def _device():
     return torch.device("cuda", torch.cuda.current_device())
 
 
+_plan_streams: dict = {}
+
+
+def _plan_stream(dev) -> "torch.cuda.Stream":
+    """The device's planner stream: the shard kernels, their read-back and the
+    pad consensus run here, not on torch's current stream, which a decode
+    pipeline makes wait for every batch in flight — so planning the next epoch
+    does not drain the pipeline."""
+    s = _plan_streams.get(dev.index)
+    if s is None:
+        s = _plan_streams[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
 def device_batch_ranges(num_rows: int, batch_size: int, rank: int, world_size: int) -> List[Range]:
     """ShardedBatchSampler ranges from the ``k_shard_ranges`` kernel."""
     dev = _device()
     ctx = _lib.get_context(dev.index)
     nb = (num_rows + batch_size - 1) // batch_size
     cap = max(1, (nb + world_size - 1) // world_size)
-    out = torch.empty((cap, 2), dtype=torch.int64, device=dev)
-    cnt = torch.zeros((1,), dtype=torch.int64, device=dev)
-    s = torch.cuda.current_stream(dev)
-    ctx.check(ctx.lib.ldt_shard_ranges(ctx.handle, num_rows, batch_size, rank, world_size,
-                                       out.data_ptr(), cap, cnt.data_ptr(), s.cuda_stream),
-              "ldt_shard_ranges")
-    n = int(cnt.item())
-    return [tuple(r) for r in out[:n].cpu().tolist()]
+    s = _plan_stream(dev)
+    with torch.cuda.stream(s):
+        out = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+        cnt = torch.zeros((1,), dtype=torch.int64, device=dev)
+        ctx.check(ctx.lib.ldt_shard_ranges(ctx.handle, num_rows, batch_size, rank, world_size,
+                                           out.data_ptr(), cap, cnt.data_ptr(), s.cuda_stream),
+                  "ldt_shard_ranges")
+        n = int(cnt.item())
+        return [tuple(r) for r in out[:n].cpu().tolist()]
 
 
 def device_fragment_batches(fragment_rows: Sequence[int], batch_size: int, rank: int,
@@ -71,19 +86,20 @@ def device_fragment_batches(fragment_rows: Sequence[int], batch_size: int, rank:
     the ``k_shard_fragments`` kernel."""
     dev = _device()
     ctx = _lib.get_context(dev.index)
-    rows = torch.tensor(list(fragment_rows), dtype=torch.int64, device=dev)
     total = sum((r + batch_size - 1) // batch_size for r in fragment_rows)
     cap = max(1, total, pad_to)
-    out = torch.empty((cap, 5), dtype=torch.int64, device=dev)
-    cnt = torch.zeros((1,), dtype=torch.int64, device=dev)
-    local = torch.zeros((1,), dtype=torch.int64, device=dev)
-    s = torch.cuda.current_stream(dev)
-    ctx.check(ctx.lib.ldt_shard_fragments(ctx.handle, rows.data_ptr() if len(fragment_rows) else None,
-                                          len(fragment_rows), batch_size, rank, world_size, pad_to,
-                                          out.data_ptr(), cap, cnt.data_ptr(), local.data_ptr(),
-                                          s.cuda_stream), "ldt_shard_fragments")
-    n = int(cnt.item())
-    return [tuple(r) for r in out[:n].cpu().tolist()], int(local.item())
+    s = _plan_stream(dev)
+    with torch.cuda.stream(s):
+        rows = torch.tensor(list(fragment_rows), dtype=torch.int64, device=dev)
+        out = torch.empty((cap, 5), dtype=torch.int64, device=dev)
+        cnt = torch.zeros((1,), dtype=torch.int64, device=dev)
+        local = torch.zeros((1,), dtype=torch.int64, device=dev)
+        ctx.check(ctx.lib.ldt_shard_fragments(ctx.handle, rows.data_ptr() if len(fragment_rows) else None,
+                                              len(fragment_rows), batch_size, rank, world_size, pad_to,
+                                              out.data_ptr(), cap, cnt.data_ptr(), local.data_ptr(),
+                                              s.cuda_stream), "ldt_shard_fragments")
+        n = int(cnt.item())
+        return [tuple(r) for r in out[:n].cpu().tolist()], int(local.item())
 
 
 def device_distributed_indices(n: int, num_replicas: int, rank: int, shuffle: bool, seed: int,
@@ -110,10 +126,17 @@ def agree_max(value: int, group=None) -> int:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return int(value)
     backend = dist.get_backend(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    return int(t.item())
+    if backend != "nccl":
+        t = torch.tensor([int(value)], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        return int(t.item())
+    # RCCL: on the planner stream, so that the collective does not queue
+    # behind the decode work torch's current stream waits for
+    dev = torch.device("cuda", torch.cuda.current_device())
+    with torch.cuda.stream(_plan_stream(dev)):
+        t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        return int(t.item())
 
 
 def _fragments(dataset):

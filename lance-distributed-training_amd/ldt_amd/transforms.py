@@ -524,11 +524,17 @@ class DecodePipeline:
     previous one — the GPU-side analogue of the reference DataLoader's
     prefetching workers (lance_map_style.py:137, num_workers=8).
 
-    Errors are asynchronous: ``check()`` waits for the most recent batch of
-    every slot and raises ImageDecodeError with its failing rows (per-image
-    status, as ldt_fetch_status reports)."""
+    Errors are asynchronous: every decode gets its context's ticket
+    (ldt_last_ticket), and ``check()`` waits for every unchecked batch and
+    raises ImageDecodeError with its failing rows (per-image status, as
+    ldt_fetch_status_ticket reports). ``check_slot(i)`` checks slot i's
+    batches older than its most recent one — a batch two uses of the slot ago,
+    long finished — so checking before each reuse never waits for the batch
+    just enqueued."""
 
     def __init__(self, depth: int = 2, device=None, profile: bool = False):
+        from collections import deque
+
         self.dec = _decoder(device)
         self.depth = max(1, int(depth))
         self.ctxs = [_lib.Context(self.dec.device.index) for _ in range(self.depth)]
@@ -537,7 +543,8 @@ class DecodePipeline:
             if profile:
                 c.set_option(_lib.OPT_PROFILE, 1)
         self.streams = [torch.cuda.Stream(self.dec.device) for _ in range(self.depth)]
-        self.sizes = [0] * self.depth
+        self.pending = [deque() for _ in range(self.depth)]  # per slot: (ticket, n), oldest first
+        self.last_ticket = None  # (slot, ticket) of the most recent decode
         self.k = 0
 
     def decode(self, batch, normalize=None, image_column: str = "image", label_column: str = "label",
@@ -553,6 +560,9 @@ class DecodePipeline:
         stream that will use the tensors, so work enqueued there in between
         (a training step) overlaps this decode (see ``prefetch``)."""
         slot = self.k % self.depth
+        # the slot's context holds the status of its last two calls: check the
+        # older one before this call replaces it (it finished long ago)
+        self.check_slot(slot)
         self.k += 1
         s = self.streams[slot]
         cur = torch.cuda.current_stream(self.dec.device)
@@ -565,12 +575,17 @@ class DecodePipeline:
         with torch.cuda.stream(s):
             out = torch.empty((n, 3, _OUT, _OUT), dtype=torch.float32, device=self.dec.device)
             lbl = torch.empty((n,), dtype=torch.int64, device=self.dec.device) if has_lbl else None
+        ctx = self.ctxs[slot]
+        before = ctx.lib.ldt_last_ticket(ctx.handle)
         if isinstance(batch, ResidentBatch):
-            batch.decode(out, lbl, normalize, ctx=self.ctxs[slot], stream=s)
+            batch.decode(out, lbl, normalize, ctx=ctx, stream=s)
         else:
             decode_arrow(images, lab, device=self.dec.device, normalize=normalize, stream=s,
-                         ctx=self.ctxs[slot], out=out, out_lbl=lbl)
-        self.sizes[slot] = n
+                         ctx=ctx, out=out, out_lbl=lbl)
+        t = ctx.lib.ldt_last_ticket(ctx.handle)
+        self.last_ticket = (slot, t) if t != before else None
+        if t != before:
+            self.pending[slot].append((t, n))
         if wait:
             cur.wait_stream(s)
             out.record_stream(cur)
@@ -605,20 +620,19 @@ class DecodePipeline:
         q = deque()
 
         def emit():
-            img, lbl, ready, slot = q.popleft()
-            # the batch's own slot is checked before it is yielded, so a bad
-            # row raises here (as PIL would) instead of reaching the consumer;
-            # it waits only for this batch, enqueued `ahead` batches ago
-            self.check_slot(slot)
+            img, lbl, ready, tk = q.popleft()
+            # the batch itself is checked before it is yielded, so a bad row
+            # raises here (as PIL would) instead of reaching the consumer; it
+            # waits only for this batch, enqueued `ahead` batches ago
+            if tk is not None:
+                self.check_ticket(*tk)
             ready()
             return _as_device_batch(img, lbl)
 
         for b in batches:
-            if self.k >= self.depth:
-                self.check_slot(self.k % self.depth)
-            slot = self.k % self.depth
+            self.check_slot(self.k % self.depth)
             q.append(self.decode(b, normalize=normalize, image_column=image_column,
-                                 label_column=label_column, wait=False) + (slot,))
+                                 label_column=label_column, wait=False) + (self.last_ticket,))
             if len(q) > ahead:
                 yield emit()
         while q:
@@ -648,27 +662,47 @@ class DecodePipeline:
         for c in self.ctxs:
             c.set_option(opt, value)
 
-    def _slot_status(self, i: int) -> dict:
-        c, s, n = self.ctxs[i], self.streams[i], self.sizes[i]
-        if n == 0:
-            return {}
+    def _ticket_status(self, i: int, ticket: int, n: int) -> dict:
+        c = self.ctxs[i]
         st = np.zeros(n, np.int32)
-        rc = c.lib.ldt_fetch_status(c.handle, s.cuda_stream, st.ctypes.data, n)
+        rc = c.lib.ldt_fetch_status_ticket(c.handle, ticket, st.ctypes.data, n)
         if rc != _lib.LDT_ERR_IMAGE:
-            c.check(rc, "ldt_fetch_status")
+            c.check(rc, "ldt_fetch_status_ticket")
         return {int(j): int(st[j]) for j in np.nonzero(st)[0]}
 
+    def check_ticket(self, i: int, ticket: int):
+        """Wait for slot i's batch `ticket` (if still unchecked); raise
+        ImageDecodeError on failures."""
+        p = self.pending[i]
+        for j, (t, n) in enumerate(p):
+            if t == ticket:
+                del p[j]
+                bad = self._ticket_status(i, t, n)
+                if bad:
+                    raise ImageDecodeError(bad)
+                return
+
     def check_slot(self, i: int):
-        """Wait for slot i's most recent batch; raise ImageDecodeError on failures."""
-        bad = self._slot_status(i)
-        self.sizes[i] = 0
-        if bad:
-            raise ImageDecodeError(bad)
+        """Check slot i's batches older than its most recent one (they finished
+        long ago: the slot's context has been used since); raise
+        ImageDecodeError on failures. Called before the slot is reused, so the
+        context's two held statuses are never overwritten unchecked."""
+        p = self.pending[i]
+        while len(p) > 1:
+            t, n = p.popleft()
+            bad = self._ticket_status(i, t, n)
+            if bad:
+                raise ImageDecodeError(bad)
 
     def check(self):
+        """Wait for every unchecked batch; raise ImageDecodeError with the
+        failing rows of all of them."""
         bad = {}
         for i in range(self.depth):
-            bad.update(self._slot_status(i))
+            p = self.pending[i]
+            while p:
+                t, n = p.popleft()
+                bad.update(self._ticket_status(i, t, n))
         if bad:
             raise ImageDecodeError(bad)
 
@@ -680,8 +714,10 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
     `depth` contexts/streams and returns at once, so batch k+1's host copy and
     kernels overlap batch k's. The tensors are ready on torch's current stream
     (it waits for the slot's stream). Per-image errors are reported
-    asynchronously: by ``fn.check()``, and at the latest when a slot is reused
-    (`depth` calls later) — unlike the synchronous ``decode_tensor_image``.
+    asynchronously: by ``fn.check()``, and at the latest when the slot is
+    reused a second time (2 * `depth` calls later, when that batch finished
+    long ago, so the check never stalls the host) — unlike the synchronous
+    ``decode_tensor_image``.
 
     ``prefetch=k`` (k < depth): ``LanceDataset`` iterates through
     ``fn.iterate`` instead, enqueueing the next k batches before yielding each
@@ -727,8 +763,7 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
 
     def to_tensor_fn(batch, **kwargs):
         maybe_register(batch, kwargs.get("image_column", image_column))
-        if pipe.k >= pipe.depth:
-            pipe.check_slot(pipe.k % pipe.depth)
+        pipe.check_slot(pipe.k % pipe.depth)
         img, lbl = pipe.decode(batch, normalize=kwargs.get("normalize", normalize),
                                image_column=kwargs.get("image_column", fixed.get("image_column", "image")),
                                label_column=kwargs.get("label_column", fixed.get("label_column", "label")))

@@ -39,6 +39,48 @@ def test_bench_json_contract(workload):
     assert 0 < roof["frac"] < 1 and abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
     ceil = roof["measured_ceiling"]
     assert 1000 < ceil["stream_copy_gbs"] < 8000
+    assert abs(d["value_per_gpu"] - d["value"] / d["n_gpus"]) <= 0.11
     if workload == "c2":
         assert d["dtype"] == "u8" and "standalone" in roof and "value_host_input" in d
         assert set(d["stages_ms_per_step"]) >= {"destuff", "huffman", "idct", "resize"}
+        # BASELINE configs[2] / configs[3] legs beside the headline
+        legs = d["config_legs"]
+        assert legs["c3"]["dataset_leg"]["sampler"] == "ShardedBatchSampler"
+        assert legs["c4"]["dataset_leg"]["sampler"] == "ShardedFragmentSampler(pad=True)"
+        for leg in legs.values():
+            assert leg["value"] > 0 and leg["per_gpu_batch"] == 128
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rehearsal():
+    """The N > 1 path of bench.py as the driver launches it (torchrun, one
+    process per rank, barriers, max over ranks, rank 0 prints one line), with
+    LDT_BENCH_BACKEND=gloo so that both ranks can share this box's one GPU."""
+    env = dict(os.environ, LDT_BENCH_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--dataset-batches", "2", "--dataset-epochs", "1"],
+                       cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["per_gpu_batch"]
+    assert abs(d["value_per_gpu"] - d["value"] / 2) <= 0.11
+    for cw, per_rank in (("c3", 2), ("c4", None)):
+        leg = d["config_legs"][cw]
+        assert leg["value_per_gpu"] * 2 == pytest.approx(leg["value"], abs=0.2)
+        info = leg["dataset_leg"]
+        assert info["images_all_ranks"] > 0 and info["epochs"] == 1
+        if per_rank:
+            # ShardedBatchSampler: every rank reads its `per_rank` batches of 128
+            assert info["images_all_ranks"] == 2 * per_rank * 128

@@ -734,3 +734,35 @@ def test_corrupt_entropy_data_is_contained(kind):
     img = ldt_amd.decode_tensor_image(_batch([base, good]))["image"].cpu().numpy()
     _check(img[0], oracle.jpeg_to_tensor(base), f"{kind}: clean batch after corrupt ones")
     _check(img[1], exp_good, f"{kind}: clean batch after corrupt ones")
+
+
+@pytest.mark.gpu
+def test_status_tickets_hold_two_calls():
+    """ldt_last_ticket / ldt_fetch_status_ticket: a context keeps the device
+    status of its last two decode calls; a batch's errors are read by ticket
+    after newer batches were enqueued, without waiting for them, and a ticket
+    older than two calls is refused."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    ctx = _lib.Context(0)
+    ctx.set_option(_lib.OPT_SYNC_STATUS, 0)
+    good = synth.encode(synth.field(64, 80, 9))
+    bad = read_golden("jpeg/bad_truncated.bin")
+    t0 = ctx.lib.ldt_last_ticket(ctx.handle)
+    tickets = []
+    for cells in ([good, bad], [good, good, good], [bad, good, good, good]):
+        ldt_amd.decode_arrow(pa.array(cells, pa.binary()), None, ctx=ctx)
+        tickets.append(ctx.lib.ldt_last_ticket(ctx.handle))
+    assert tickets == [t0 + 1, t0 + 2, t0 + 3]
+    torch.cuda.synchronize()
+    st = np.zeros(4, np.int32)
+    # the first call's status is gone (two newer calls), the others are held
+    assert ctx.lib.ldt_fetch_status_ticket(ctx.handle, tickets[0], st.ctypes.data, 2) == _lib.LDT_ERR_ARG
+    assert ctx.lib.ldt_fetch_status_ticket(ctx.handle, tickets[1], st.ctypes.data, 3) == _lib.LDT_OK
+    assert st[:3].tolist() == [0, 0, 0]
+    st[:] = 0
+    assert ctx.lib.ldt_fetch_status_ticket(ctx.handle, tickets[2], st.ctypes.data, 4) == _lib.LDT_ERR_IMAGE
+    assert st.tolist() == [3, 0, 0, 0]
