@@ -208,7 +208,7 @@ def main():
     ap.add_argument("--dataset-epochs", type=int, default=2,
                     help="epochs in the dataset leg's timed region (each re-plans, as a training loop does)")
     ap.add_argument("--resize-impl", type=int, default=0,
-                    help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize420 for 4:2:0; 1 k_resize4)")
+                    help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize4; 3 k_resize420 for 4:2:0)")
     ap.add_argument("--no-config-legs", action="store_true",
                     help="skip the configs[2]/configs[3] dataset legs (c3, c4) of a c2 run")
     ap.add_argument("--registered", action="store_true",

@@ -328,44 +328,22 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
 // registers: a block's coefficient indices only grow, so a group is complete
 // once the decode moves to another group or block. Only nonzero groups are
 // stored, packed (ldt_kernels.hpp): one 16-byte unit each, consecutive for the
-// run's consecutive blocks, and four units (one 64-byte segment) leave
-// together, so that a segment reaches the L2 as one burst from one lane.
-__device__ __forceinline__ void store_units(uint4 *__restrict__ p, const uint4 &a, const uint4 &b,
-                                            const uint4 &c, const uint4 &d) {
-  p[0] = a;
-  p[1] = b;
-  p[2] = c;
-  p[3] = d;
-}
-
-// q0 <- q1 <- q2 <- q3 <- x when p (the unit queue of write_run).
-__device__ __forceinline__ uint32_t sel(bool p, uint32_t a, uint32_t b) { return p ? a : b; }
-__device__ __forceinline__ void shift_in(bool p, uint4 &q0, uint4 &q1, uint4 &q2, uint4 &q3, const uint4 &x) {
-  q0.x = sel(p, q1.x, q0.x); q0.y = sel(p, q1.y, q0.y); q0.z = sel(p, q1.z, q0.z); q0.w = sel(p, q1.w, q0.w);
-  q1.x = sel(p, q2.x, q1.x); q1.y = sel(p, q2.y, q1.y); q1.z = sel(p, q2.z, q1.z); q1.w = sel(p, q2.w, q1.w);
-  q2.x = sel(p, q3.x, q2.x); q2.y = sel(p, q3.y, q2.y); q2.z = sel(p, q3.z, q2.z); q2.w = sel(p, q3.w, q2.w);
-  q3.x = sel(p, x.x, q3.x); q3.y = sel(p, x.y, q3.y); q3.z = sel(p, x.z, q3.z); q3.w = sel(p, x.w, q3.w);
-}
+// run's consecutive blocks. (Holding four units back in registers so that a
+// run's 64-byte segments leave as one burst cut the kernel's HBM writes from
+// ~210 to 132 MB per c2 batch but made the write pass 20 us per image slower:
+// the extra store instructions issue for the whole wave)
 
 // Where a run's block records and chunk carries go: the workgroup's LDS
 // (k_huff_image, copied out coalesced after the DC scan) or global memory.
-// put_if: the LDS sink stores unconditionally (to a scratch word when `p` is
-// false), which keeps the write loop free of branches around it.
 struct RecLds {
-  LDS_AS uint32_t *rec, *carry, *scratch;
+  LDS_AS uint32_t *rec, *carry;
   __device__ __forceinline__ void put(int ib, uint32_t v) const { rec[ib] = v; }
-  __device__ __forceinline__ void put_if(bool p, int ib, uint32_t v) const { *(p ? rec + ib : scratch) = v; }
-  __device__ __forceinline__ void carry_if(bool p, int c, uint32_t u) const { *(p ? carry + c : scratch) = u; }
+  __device__ __forceinline__ void put_carry(int c, uint32_t u) const { carry[c] = u; }
 };
 struct RecGlob {
   uint32_t *rec, *carry;
   __device__ __forceinline__ void put(int ib, uint32_t v) const { rec[ib] = v; }
-  __device__ __forceinline__ void put_if(bool p, int ib, uint32_t v) const {
-    if (p) rec[ib] = v;
-  }
-  __device__ __forceinline__ void carry_if(bool p, int c, uint32_t u) const {
-    if (p) carry[c] = u;
-  }
+  __device__ __forceinline__ void put_carry(int c, uint32_t u) const { carry[c] = u; }
 };
 
 // Coefficient-writing decode of one range, with block ownership: a block
@@ -377,26 +355,25 @@ struct RecGlob {
 // [0, lim) (lim: the segment's blocks not started before the range); the run
 // ends before a block beyond lim. Its nonzero groups are packed from unit
 // 8 * base of the image's coefficient region (at most 8 per block, so a run
-// never reaches the next run's units; 8 * base is segment-aligned). Each
-// block's record (gmask | run start << 8 | DC difference << 16, see
-// ldt_kernels.hpp) is stored when the next block starts or the run ends, and
-// a block at a multiple of 64 publishes its first unit as its chunk's carry.
-// The loop has one group site: the buffered group joins the unit queue when a
-// nonzero AC value opens another group or a block starts.
+// never reaches the next run's units). Each block's record (gmask | run
+// start << 8 | DC difference << 16, see ldt_kernels.hpp) is stored when the
+// next block starts or the run ends, and a block at a multiple of 64
+// publishes its first unit as its chunk's carry. The loop has one group store
+// site: the buffered group is stored when a nonzero AC value opens another
+// group or a block starts.
 template <class W, class RS>
 __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
                                           int &cursor, int lim, uint4 *__restrict__ coef_img,
                                           const RS &rs, int base) {
   uint64_t lo = 0, hi = 0;           // buffered group: slots 0-3, 4-7
   int cg = -1;                       // its group index; < 0: none
-  uint4 q0 = make_uint4(0u, 0u, 0u, 0u), q1 = q0, q2 = q0, q3 = q0; // the segment's units (q3 newest)
-  uint32_t wu = (uint32_t)base * 8u; // units stored or queued
+#if defined(LDT_EXP_WR_Q2)
+  uint4 q2 = make_uint4(0u, 0u, 0u, 0u), q3 = q2;
+#endif
+  uint32_t wu = (uint32_t)base * 8u; // units stored
   uint32_t gmask = 0;                // groups of the current block
   uint32_t dcd = 0;                  // its DC difference (16 bits)
   bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
-  // Branch-free bookkeeping (selects, predicated LDS stores): a wave's lanes
-  // take the group and block paths at different symbols, so branches around
-  // them would be executed by the whole wave at almost every symbol anyway.
   while (go) {
     const bool first = st.k == 0; // a block starts: its DC symbol
     const uint32_t pk = R.peek();
@@ -409,43 +386,35 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     const int g = slot >> 3;
     const bool opens = !first && v != 0 && g != cg && cursor >= 0;
     const bool flush = cg >= 0 && (first || opens);
-    // component-wise selects (a select of whole uint4 values becomes a
-    // select of their addresses in scratch memory)
     const uint4 cur = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-#if defined(LDT_EXP_WR_NOQ)
+#if defined(LDT_EXP_WR_Q2)
     if (flush) {
-      coef_img[wu] = cur;
-      gmask |= 1u << cg;
-      ++wu;
-    }
-#elif defined(LDT_EXP_WR_QBRANCH)
-    if (flush) {
-      q0 = q1;
-      q1 = q2;
       q2 = q3;
       q3 = cur;
       gmask |= 1u << cg;
       ++wu;
-      if ((wu & 3u) == 0) store_units(coef_img + (wu - 4), q0, q1, q2, q3);
+      if ((wu & 1u) == 0) {
+        coef_img[wu - 2] = q2;
+        coef_img[wu - 1] = q3;
+      }
     }
 #else
-    shift_in(flush, q0, q1, q2, q3, cur);
-    gmask |= flush ? 1u << (cg & 7) : 0u;
-    wu += flush ? 1u : 0u;
-    if (flush && (wu & 3u) == 0) store_units(coef_img + (wu - 4), q0, q1, q2, q3);
+    if (flush) {
+#ifdef LDT_EXP_WR_NT
+      __builtin_nontemporal_store((v4u){cur.x, cur.y, cur.z, cur.w}, reinterpret_cast<v4u *>(coef_img + wu));
+#else
+      coef_img[wu] = cur;
+#endif
+      gmask |= 1u << cg;
+      ++wu;
+    }
 #endif
     // a block starts: the previous one's record, then this block's state
-#ifdef LDT_EXP_WR_RBRANCH
     if (first) {
       if (cursor >= 0) rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
       ++cursor;
-      if (((base + cursor) & 63) == 0) rs.carry_if(true, (base + cursor) >> 6, wu);
+      if (((base + cursor) & 63) == 0) rs.put_carry((base + cursor) >> 6, wu);
     }
-#else
-    rs.put_if(first && cursor >= 0, base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
-    cursor += first ? 1 : 0;
-    rs.carry_if(first && ((base + cursor) & 63) == 0, (base + cursor) >> 6, wu);
-#endif
     gmask = first ? 0u : gmask;
     dcd = first ? (uint32_t)v & 0xFFFFu : dcd;
     lo = (first || opens) ? 0ull : lo;
@@ -460,37 +429,23 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   }
   if (cursor >= 0) {
-    bool last = false; // the buffered group of the last block joined the queue
     if (cg >= 0) {
-      q0 = q1;
-      q1 = q2;
-      q2 = q3;
-      q3 = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+      const uint4 cur = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+#if defined(LDT_EXP_WR_Q2)
+      if (wu & 1u) {
+        coef_img[wu - 1] = q3;
+      }
+#endif
+      coef_img[wu] = cur;
       gmask |= 1u << cg;
       ++wu;
-      last = true;
     }
-    rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
-#ifdef LDT_EXP_WR_NOQ
-    if (last) coef_img[wu - 1] = q3;
-    return;
+#if defined(LDT_EXP_WR_Q2)
+    else if (wu & 1u) {
+      coef_img[wu - 1] = q3;
+    }
 #endif
-    // the queued units not stored yet: the newest (wu & 3) of q0..q3, or all
-    // four when that last group completed a segment
-    const uint32_t k = wu & 3u;
-    uint4 *p = coef_img + (wu - k);
-    if (k == 0 && last) {
-      store_units(coef_img + (wu - 4), q0, q1, q2, q3);
-    } else if (k == 3) {
-      p[0] = q1;
-      p[1] = q2;
-      p[2] = q3;
-    } else if (k == 2) {
-      p[0] = q2;
-      p[1] = q3;
-    } else if (k == 1) {
-      p[0] = q3;
-    }
+    rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
   }
 }
 
@@ -785,7 +740,6 @@ struct ImgLds {
     struct {
       uint32_t rec[kRecCap];
       uint32_t carry[kRecCap / 64];
-      uint32_t rec_scratch; // target of the write loop's predicated-off stores
     };
   };
   int32_t seg_first[kMaxParSegs + 1]; // sub_first of the image's segments; [nseg] = slots
@@ -1064,8 +1018,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
     if (rec_lds)
       write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
-                RecLds{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry, (LDS_AS uint32_t *)&sh.rec_scratch},
-                base);
+                RecLds{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry}, base);
     else
       write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
                 RecGlob{brec + d.coef_off, bcarry + d.coef_off / 64}, base);

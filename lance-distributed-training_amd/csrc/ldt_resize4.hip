@@ -179,11 +179,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   // kernel is LDS-bound). JPEG rows stay plain: the skew's extra registers
   // cost a wave per SIMD there, which is worth more than its 2-way conflicts.
   constexpr bool kJpeg = SRC == 0 || SRC == 2;
-#ifdef LDT_EXP_JPEG_SKEW
-  constexpr bool kSkew = true;
-#else
   constexpr bool kSkew = !kJpeg;
-#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
   for (int i = tid; i < 768; i += (int)blockDim.x) s_lut[i] = lut[i];
@@ -497,9 +493,6 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
           f.y = lc[min((uint32_t)acc[i][1] >> kPrecisionBits, 255u)];
           f.z = lc[min((uint32_t)acc[i][2] >> kPrecisionBits, 255u)];
           f.w = lc[min((uint32_t)acc[i][3] >> kPrecisionBits, 255u)];
-#ifdef LDT_EXP_NOSTORE
-          if (f.x + f.y + f.z + f.w == 12345.f)
-#endif
           *reinterpret_cast<float4 *>(out + (((int64_t)img * 3 + vc[i]) * kOut + oy0 + j) * kOut + vo[i]) = f;
         }
       }
@@ -516,15 +509,9 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   fetch(pa, ya0);
   for (int y = ya0; y < yb; y += 2) {
     stage(pa, y);
-#ifdef LDT_EXP_STORE_FIRST
-    wave_lds_fence();
-    vertical(y);
-    if (y + 2 < yb) fetch(pa, y + 2);
-#else
     if (y + 2 < yb) fetch(pa, y + 2);
     wave_lds_fence();
     vertical(y);
-#endif
     horizontal(y);
     wave_lds_fence();
   }
@@ -532,7 +519,8 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
 }
 
 // ---------------------------------------------------------------------------
-// k_resize420: the 4:2:0 fast path (resize_fast420 images) with TWO waves per
+// k_resize420 (LDT_OPT_RESIZE_IMPL 3; measured slower than k_resize4, see
+// DESIGN.md §4): the 4:2:0 fast path (resize_fast420 images) with TWO waves per
 // (image, band) task. Per source row pair the waves stage one row each (wave
 // w: row y + w, 8 luma pixels per lane, h2v2 fancy upsampling + YCbCr->RGB in
 // registers) into the workgroup's shared, skewed staging rows; after a
