@@ -211,8 +211,11 @@ def main():
                     help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize4; 3 k_resize420 for 4:2:0)")
     ap.add_argument("--no-config-legs", action="store_true",
                     help="skip the configs[2]/configs[3] dataset legs (c3, c4) of a c2 run")
-    ap.add_argument("--registered", action="store_true",
-                    help="also time the host leg with the cell buffers page-locked in place (ldt_register_host)")
+    ap.add_argument("--no-registered", action="store_true",
+                    help="skip the host leg with the cell buffers page-locked in place (ldt_register_host)")
+    ap.add_argument("--dataset-copy", action="store_true",
+                    help="dataset legs through the copying to_tensor_fn instead of registering the mapped "
+                         "fragments' image buffers")
     args = ap.parse_args()
 
     import numpy as np
@@ -340,7 +343,7 @@ def main():
     value_host = value_registered = host_us = None
     if args.workload != "c5":
         value_host, host_us = host_rate(host_batches)
-        if args.registered:
+        if not args.no_registered:
             try:
                 value_registered, _ = host_rate(host_batches, register=True)
             except ldt_amd.LdtError as e:
@@ -436,7 +439,9 @@ def main():
         res["value_host_input_per_gpu"] = round(value_host / world, 1)
         res["value_host_input_note"] = ("the same steps with the cells in host pa.RecordBatches through the "
                                         "pipelined to_tensor_fn (make_to_tensor_fn(depth)): pinned copy "
-                                        "overlapped with the header walk + H2D every step")
+                                        "overlapped with the header walk + H2D every step; "
+                                        "value_host_registered: the same with the two batches' image buffers "
+                                        "page-locked in place (register=True), DMA without the host copy")
         res["host_us_per_call"] = host_us
     if value_registered is not None:
         res["value_host_registered"] = round(value_registered, 1)
@@ -463,9 +468,8 @@ def main():
     tr = load_profile(f"traffic_{args.workload}.json")
     if tr is not None and tr.get("batch", B) == B:
         res["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
-        res["roofline"]["traffic_source"] = (f"profiles/{PROFILE_ROUND}/traffic_{args.workload}.json: rocprofv3 "
-                                             "--pmc FETCH_SIZE and WRITE_SIZE passes (FETCH_SIZE x2, gfx950) "
-                                             "over this bench at depth 1")
+        res["roofline"]["traffic_source"] = (f"{tr['source']}: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE "
+                                             "passes (FETCH_SIZE x2, gfx950) over this bench at depth 1")
     dec = load_profile(f"pmc_{args.workload}_decode.json")
     if dec is not None:
         res["decode_efficiency"] = dec
@@ -537,7 +541,10 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
         sampler = ldt_amd.ShardedFragmentSampler(rank=rank, world_size=world, pad=True)
     else:
         sampler = ldt_amd.ShardedBatchSampler(rank=rank, world_size=world)
-    fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev)
+    # the fragments are memory-mapped Arrow IPC files whose image buffers live
+    # as long as the dataset: page-locked once per fragment (register=True),
+    # every batch sliced from them is DMAed without a host copy
+    fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev, register=not args.dataset_copy)
     fn.pipeline.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
     ds = ldt_amd.LanceDataset(path, batch_size=B, sampler=sampler, to_tensor_fn=fn)
 
@@ -572,11 +579,12 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
             "images_all_ranks": tot_imgs, "elapsed_ms_max": round(t * 1e3, 3),
             "timing": "full epochs per rank (plan + every batch, padding included) between barriers, "
                       "max over ranks",
-            "harness": "LanceDataset(path, batch_size, sampler, to_tensor_fn=make_to_tensor_fn(depth))"}
+            "harness": ("LanceDataset(path, batch_size, sampler, to_tensor_fn=make_to_tensor_fn(depth, "
+                        f"register={not args.dataset_copy}))")}
     return tot_imgs / t, info
 
 
-PROFILE_ROUND = "r2"
+PROFILE_ROUND = "r3"  # committed PMC summaries: this round's, else the newest earlier one
 
 
 def stream_copy_ceiling(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
@@ -602,12 +610,18 @@ def stream_copy_ceiling(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
 
 
 def load_profile(name: str):
-    """A committed PMC summary under profiles/<round>/ (None if absent)."""
-    path = os.path.join(REPO, "profiles", PROFILE_ROUND, name)
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        return json.load(f)
+    """A committed PMC summary under profiles/<round>/ — this round's, else the
+    newest earlier round's (None if absent); the dict gains its source path."""
+    rnd = int(PROFILE_ROUND[1:])
+    for r in range(rnd, 0, -1):
+        path = os.path.join(REPO, "profiles", f"r{r}", name)
+        if os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            if isinstance(d, dict):
+                d.setdefault("source", os.path.relpath(path, REPO))
+            return d
+    return None
 
 
 def ldt_amd_dims(cell: bytes):

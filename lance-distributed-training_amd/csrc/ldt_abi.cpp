@@ -566,6 +566,20 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   std::unordered_map<std::string, int> ptab_map;
   std::vector<int32_t> prog_img;
   bool any_bad = false;
+  // The tables of the previous image (per component): images of one dataset
+  // mostly share their DQT/DHT bytes, so a byte compare against the last
+  // match skips the key strings and hash lookups of the dedupe below.
+  struct LastQ {
+    uint16_t q[64];
+    int idx = -1;
+  } last_q[3];
+  struct LastH {
+    RawHuff r;
+    int bidx = -1;
+  } last_h[3][2];
+  auto same_huff = [](const RawHuff &a, const RawHuff &b) {
+    return a.nsym == b.nsym && memcmp(a.counts, b.counts, 16) == 0 && memcmp(a.syms, b.syms, (size_t)a.nsym) == 0;
+  };
   for (int64_t i = 0; i < n; ++i) {
     ImgPlan &ip = P[(size_t)i];
     ImgDesc &d = D[(size_t)i];
@@ -675,16 +689,28 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
       }
       // quant table (progressive: latched at the component's first scan)
       const uint16_t *qsrc = H.progressive ? PP.q[k] : H.q[H.tq[k]];
-      std::string qk(reinterpret_cast<const char *>(qsrc), 128);
-      auto qi = qmap.find(qk);
-      if (qi == qmap.end()) {
-        qi = qmap.emplace(qk, (int)qtabs.size()).first;
-        qtabs.emplace_back(qsrc, qsrc + 64);
+      if (last_q[k].idx >= 0 && memcmp(last_q[k].q, qsrc, 128) == 0) {
+        d.qt[k] = last_q[k].idx;
+      } else {
+        std::string qk(reinterpret_cast<const char *>(qsrc), 128);
+        auto qi = qmap.find(qk);
+        if (qi == qmap.end()) {
+          qi = qmap.emplace(qk, (int)qtabs.size()).first;
+          qtabs.emplace_back(qsrc, qsrc + 64);
+        }
+        d.qt[k] = qi->second;
+        memcpy(last_q[k].q, qsrc, 128);
+        last_q[k].idx = d.qt[k];
       }
-      d.qt[k] = qi->second;
       // Huffman tables (deduped across the context's lifetime)
       for (int pass = 0; pass < 2 && !H.progressive; ++pass) {
         const RawHuff &rh = pass == 0 ? H.dc[H.td[k]] : H.ac[H.ta[k]];
+        LastH &lh = last_h[k][pass];
+        if (lh.bidx >= 0 && same_huff(lh.r, rh)) {
+          if (pass == 0) d.dct[k] = lh.bidx;
+          else d.act[k] = lh.bidx;
+          continue;
+        }
         std::string key = huff_key(rh, pass == 0);
         auto it = c->hmap.find(key);
         int cid;
@@ -711,6 +737,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
         }
         if (pass == 0) d.dct[k] = bidx;
         else d.act[k] = bidx;
+        lh.r = rh;
+        lh.bidx = bidx;
       }
     }
     if (ip.status != LDT_IMG_OK) {

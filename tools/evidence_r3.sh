@@ -15,7 +15,7 @@ cd $R
 if [ "$2" = "A" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -20 $O/pytest_gpu.log; exit 1; }
   tail -1 $O/pytest_gpu.log
-  timeout -k 10 500 python bench.py --registered > $O/bench_c2.json 2> $O/bench_c2.err || { tail -5 $O/bench_c2.err; exit 1; }
+  timeout -k 10 500 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { tail -5 $O/bench_c2.err; exit 1; }
   echo "c2: $(head -c 200 $O/bench_c2.json)"
   timeout -k 10 120 python3 tools/probes/huff_rounds.py > $O/huff_rounds.txt 2>&1 || exit 1
   cd /tmp && export TMPDIR=/tmp

@@ -1,7 +1,8 @@
 """Diagnostic (not a test): one leg of the c2 bench for a rocprofv3
 --kernel-trace --memory-copy-trace run: 'host' = host RecordBatches through the
-pipelined to_tensor_fn (the bench's host leg), 'resident' = ResidentBatches
-through DecodePipeline. usage: host_trace.py host|resident [depth]"""
+pipelined to_tensor_fn (the bench's host leg), 'reg' = the same with the
+batches' image buffers page-locked in place (register=True), 'resident' = ResidentBatches
+through DecodePipeline. usage: host_trace.py host|reg|resident [depth]"""
 import os
 import sys
 import time
@@ -22,13 +23,13 @@ dev = torch.device("cuda", 0)
 bs = []
 for k in range(2):
     cells, labels = make_cells("c2", 256, seed=k)
-    if leg == "host":
+    if leg in ("host", "reg"):
         bs.append(pa.RecordBatch.from_arrays([pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
                                              names=["image", "label"]))
     else:
         bs.append(ldt_amd.ResidentBatch(cells, labels, device=dev))
-if leg == "host":
-    fn = ldt_amd.make_to_tensor_fn(depth=depth, device=dev)
+if leg in ("host", "reg"):
+    fn = ldt_amd.make_to_tensor_fn(depth=depth, device=dev, register=leg == "reg")
     step = lambda b: fn(b)  # noqa: E731
 else:
     pipe = ldt_amd.DecodePipeline(depth=depth, device=dev)
