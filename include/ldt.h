@@ -77,7 +77,7 @@ extern "C" {
 #define LDT_OPT_COPY_THREADS 8 /* threads of the context's host copy pool that
                                  move a batch's cells into the pinned slot while
                                  the calling thread walks the headers (0..31;
-                                 -1 = default, min(4, cores - 1))             */
+                                 -1 = default, min(6, cores - 2))             */
 #define LDT_OPT_HOST_TIMING 9 /* 1: accumulate host phase times of every
                                  decode call (read with ldt_host_times)        */
 #define LDT_OPT_RESIZE_WAVES_PCT 10 /* resize bands per batch as % of one full

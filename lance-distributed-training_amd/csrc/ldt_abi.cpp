@@ -200,7 +200,7 @@ struct ldt_ctx {
   int warm_pct = 0;
   int subseq_bits = 256; // minimum S of the parallel decoder
   int resize_waves_pct = 100;
-  int copy_threads = -1; // -1: default (min(4, cores - 1))
+  int copy_threads = -1; // -1: default (min(6, cores - 2))
   bool host_timing = false;
   DevBuf d_data, d_plan, d_dstuf, d_coef, d_brec, d_bcarry, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt;
   DevBuf d_perm; // DistributedSampler scratch: 3 int32 arrays of dataset_len
