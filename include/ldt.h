@@ -84,6 +84,11 @@ extern "C" {
                                  wave of resize waves on the device (10..1000,
                                  default 100); more bands fill the pipeline's
                                  CU gaps, fewer keep the kernel efficient      */
+#define LDT_OPT_FUSED_DESTUFF 11 /* 1 (default): the parallel Huffman decoder
+                                 destuffs the scan bytes of an image whose
+                                 stream fits its LDS window itself; 0: every
+                                 image through the k_destuff_* kernels
+                                 (cross-check)                                  */
 
 /* ---- stages reported by ldt_stage_times ---- */
 #define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */

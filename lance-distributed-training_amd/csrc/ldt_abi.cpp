@@ -191,6 +191,10 @@ enum HostPhase {
   kHpCount
 };
 
+#ifndef LDT_FUSE_DEFAULT
+#define LDT_FUSE_DEFAULT true // experiment builds: -DLDT_FUSE_DEFAULT=false
+#endif
+
 struct ldt_ctx {
   int device = 0;
   std::string err;
@@ -200,6 +204,7 @@ struct ldt_ctx {
   int warm_pct = 0;
   int subseq_bits = 256; // minimum S of the parallel decoder
   int resize_waves_pct = 100;
+  bool fuse_destuff = LDT_FUSE_DEFAULT; // LDT_OPT_FUSED_DESTUFF
   int copy_threads = -1; // -1: default (min(6, cores - 2))
   bool host_timing = false;
   DevBuf d_data, d_plan, d_dstuf, d_coef, d_brec, d_bcarry, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt;
@@ -863,6 +868,31 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     if (kv > max_ks_v) max_ks_v = kv;
   }
 
+  // Fused destuff: a k_huff_image workgroup whose image's destuffed stream
+  // fits its LDS window destuffs the scan bytes itself (ldt_huffman.hip
+  // destuff_into_window); those images get no destuff chunks (ds_count 0)
+  int n_ds_img = 0; // baseline images left to k_destuff_*
+  {
+    const int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs);
+    const int64_t winb = std::min<int64_t>(max_window, cap) & ~(int64_t)15;
+    chunk_img.clear();
+    n_chunks = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      ImgDesc &d = D[(size_t)i];
+      d.ds_first = n_chunks;
+      if (st[(size_t)i] != LDT_IMG_OK || d.nseg == 0) {
+        d.ds_count = 0;
+        continue;
+      }
+      const bool fused = c->fuse_destuff && d.sub_bits > 0 &&
+                         destuff_region_bytes(d.src_len, d.nseg) + 16 <= winb;
+      d.ds_count = fused ? 0 : (int32_t)((d.src_len + 3 + kDsChunkBytes - 1) / kDsChunkBytes);
+      for (int q = 0; q < d.ds_count; ++q) chunk_img.push_back((int32_t)i);
+      n_chunks += d.ds_count;
+      n_ds_img += fused ? 0 : 1;
+    }
+  }
+
   ht.mark(kHpParse); // headers parsed, per-image plans built
   // ---- plan blob layout ----
   PlanHdr ph;
@@ -981,6 +1011,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.resize_waves_pct = c->resize_waves_pct;
   p.resize420 = c->resize_impl == 3 ? 1 : 0;
   p.n_chunks = n_chunks;
+  p.n_ds_img = n_ds_img;
   p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
   p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
   p.max_tabs = max_tabs;
@@ -1203,6 +1234,9 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
   case LDT_OPT_RESIZE_WAVES_PCT:
     if (value < 10 || value > 1000) return set_err(c, LDT_ERR_ARG, "resize waves %lld%%", (long long)value);
     c->resize_waves_pct = (int)value;
+    return LDT_OK;
+  case LDT_OPT_FUSED_DESTUFF:
+    c->fuse_destuff = value != 0;
     return LDT_OK;
   default:
     return set_err(c, LDT_ERR_ARG, "unknown option %d", option);

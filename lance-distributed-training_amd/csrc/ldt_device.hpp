@@ -152,4 +152,112 @@ __device__ __forceinline__ void ycc_to_rgb(int Y, int cb, int cr, uint8_t *o) {
   o[2] = (uint8_t)clampi(Y + cb_b, 0, 255);
 }
 
+
+// Destuff classification of 16 bytes (jdhuff.c jpeg_fill_bit_buffer /
+// jdmarker.c semantics): wv[1..4] hold them, wv[0] and wv[5] the words on
+// either side; p0 is the position of the first one relative to the scan start
+// and L the scan's length. keep: bytes kept (FF00 -> FF, fill bytes and marker
+// bytes dropped); rst: RSTn codes (segment boundaries); local_end: index of an
+// end-of-scan marker's FF (16: none).
+__host__ __device__ __forceinline__ void ds_classify16(const uint32_t wv[6], int64_t p0, int64_t L,
+                                              uint32_t &keep, uint32_t &rst, int &local_end) {
+  keep = rst = 0;
+  local_end = 16;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t p = p0 + j;
+    const uint32_t prev = (wv[(j + 3) >> 2] >> (8 * ((j + 3) & 3))) & 255;
+    const uint32_t cur = (wv[(j + 4) >> 2] >> (8 * ((j + 4) & 3))) & 255;
+    const uint32_t next = (wv[(j + 5) >> 2] >> (8 * ((j + 5) & 3))) & 255;
+    const bool in = p >= 0 && p < L;
+    const bool next_in = p + 1 < L;
+    bool drop = false;
+    if (cur == 0xFF) {
+      const uint32_t nx = next_in ? next : 0u;
+      if (nx == 0x00) {
+        drop = false;                        // stuffed data byte 0xFF
+      } else if (nx == 0xFF || (nx >= 0xD0 && nx <= 0xD7)) {
+        drop = true;                         // fill byte or RSTn prefix
+      } else if (in && next_in) {
+        if (local_end == 16) local_end = j;  // end-of-scan marker
+        drop = true;
+      } else {
+        drop = true;                         // trailing 0xFF at end of cell
+      }
+    } else if (prev == 0xFF && p > 0) {
+      if (cur == 0x00) drop = true;          // stuffing zero
+      else if (cur >= 0xD0 && cur <= 0xD7) {
+        drop = true;
+        if (in) rst |= 1u << j;              // RSTn code: segment boundary
+      }
+    }
+    if (in && !drop) keep |= 1u << j;
+  }
+}
+
+
+// The same classification driven by the 0xFF bytes (k_huff_image's fused
+// destuff): every byte is kept unless it is an 0xFF or follows one, so the
+// lane finds its 0xFF bytes with a word-parallel test and applies the rules
+// above only around them (one or two per 16 bytes of entropy-coded data at
+// most, usually none) instead of testing all 16 bytes.
+__host__ __device__ __forceinline__ uint32_t ds_ff4(uint32_t w) { // bit i: byte i == 0xFF
+  const uint32_t t = ~w;
+  const uint32_t h = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+  return (((h >> 7) * 0x204081u) >> 21) & 0xFu;
+}
+__host__ __device__ __forceinline__ uint32_t ds_byte(const uint32_t wv[6], int k) { // k < 24
+  const int q = k >> 2;
+  uint32_t w = wv[0];
+  w = q == 1 ? wv[1] : w;
+  w = q == 2 ? wv[2] : w;
+  w = q == 3 ? wv[3] : w;
+  w = q == 4 ? wv[4] : w;
+  w = q == 5 ? wv[5] : w;
+  return (w >> (8 * (k & 3))) & 255u;
+}
+__host__ __device__ __forceinline__ void ds_classify16_ff(const uint32_t wv[6], int64_t p0, int64_t L,
+                                                          uint32_t &keep, uint32_t &rst, int &local_end) {
+  // bytes j in [lo, hi) lie in the scan
+  const int lo = p0 >= 0 ? 0 : (p0 <= -16 ? 16 : (int)-p0);
+  const int64_t room = L - p0;
+  const int hi = room <= 0 ? 0 : (room >= 16 ? 16 : (int)room);
+  keep = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
+  rst = 0;
+  local_end = 16;
+  uint32_t ff = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) ff |= ds_ff4(wv[i]) << (4 * i);
+  // 0xFF bytes from the one before the lane's first (bit 0) to its last (16)
+  uint32_t m = (ff >> 3) & 0x1FFFFu;
+  while (m) {
+    const int b = __builtin_ctz(m);
+    m &= m - 1u;
+    const int j = b - 1; // the 0xFF's byte (-1: the previous lane's last)
+    const uint32_t nx_raw = ds_byte(wv, b + 4);
+    if (j >= 0) {
+      const int64_t p = p0 + j;
+      const bool in = p >= 0 && p < L;
+      const bool next_in = p + 1 < L;
+      const uint32_t nx = next_in ? nx_raw : 0u;
+      if (nx != 0u) { // not a stuffed 0xFF: dropped
+        keep &= ~(1u << j);
+        const bool fill_rst = nx == 0xFFu || (nx >= 0xD0u && nx <= 0xD7u);
+        if (!fill_rst && in && next_in && j < local_end) local_end = j; // end-of-scan marker
+      }
+    }
+    // the byte after it, unless that is an 0xFF itself (its own rule)
+    const int j1 = j + 1;
+    if (j1 <= 15 && nx_raw != 0xFFu && p0 + j1 > 0) {
+      if (nx_raw == 0u) {
+        keep &= ~(1u << j1); // stuffing zero
+      } else if (nx_raw >= 0xD0u && nx_raw <= 0xD7u) {
+        keep &= ~(1u << j1); // RSTn code: segment boundary
+        const int64_t p1 = p0 + j1;
+        if (p1 >= 0 && p1 < L) rst |= 1u << j1;
+      }
+    }
+  }
+}
+
 } // namespace ldt

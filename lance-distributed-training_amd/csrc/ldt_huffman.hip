@@ -108,6 +108,20 @@ struct Rd {
     wi += m ? 1 : 0;
     nxt = src(wi);
   }
+  // consume() without the refill: the caller reloads nxt with refill() at the
+  // top of its next step, next to the lookup, so that both LDS loads share
+  // one wait (a refill at the end of a loop body with branches is waited for
+  // on the spot to merge its value)
+  __device__ __forceinline__ void consume_nl(int t) {
+    p += t;
+    const int32_t r2 = rs - t;
+    const bool m = r2 < 0;
+    hi = m ? lo : hi;
+    lo = m ? nxt : lo;
+    rs = r2 & 31;
+    wi += m ? 1 : 0;
+  }
+  __device__ __forceinline__ void refill() { nxt = src(wi); }
 };
 
 // ---------------------------------------------------------------------------
@@ -375,6 +389,9 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
   uint32_t dcd = 0;                  // its DC difference (16 bits)
   bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   while (go) {
+#ifndef LDT_EXP_OLDREFILL
+    R.refill();
+#endif
     const bool first = st.k == 0; // a block starts: its DC symbol
     const uint32_t pk = R.peek();
     const uint32_t e = lookup(dec, st, pk);
@@ -424,7 +441,11 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     const uint64_t x = cg >= 0 ? (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3)) : 0ull;
     lo |= (slot & 4) ? 0ull : x;
     hi |= (slot & 4) ? x : 0ull;
+#ifndef LDT_EXP_OLDREFILL
+    R.consume_nl((int)(e & 31));
+#else
     R.consume((int)(e & 31));
+#endif
     advance(st, dec, adv);
     go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   }
@@ -747,6 +768,7 @@ struct ImgLds {
   int32_t seg_nb[kMaxParSegs];        // segment length in bits
   int32_t scan[kHuffThreads / 64];
   int32_t any_changed;
+  int32_t ds_end; // fused destuff: scan position of the end-of-scan marker
   int32_t need_lanes, need_waves, memo_hits; // diagnostic counters (summed over rounds)
 };
 static_assert(sizeof(ImgLds) + 512 <= kHuffStaticLds, "k_huff_image static LDS");
@@ -992,7 +1014,8 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   const Segment &sg = segs[d.seg_base + g.si];
   // the write pass ends where the next range starts: this lane's exit (a
   // count step may run past the range end); a segment's last range at its end
-  const int32_t wstop = g.j == sg.sub_count - 1 ? g.stop : g.pbias + sh.ex_p[tid];
+  const int sub_count = sh.seg_first[g.si + 1] - sh.seg_first[g.si];
+  const int32_t wstop = g.j == sub_count - 1 ? g.stop : g.pbias + sh.ex_p[tid];
   int tot;
   const int pre = block_excl_scan1024(live ? (int)sh.nblk[tid] : 0, sh.scan, &tot);
   sh.ex_p[tid] = pre;
@@ -1022,7 +1045,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     else
       write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
                 RecGlob{brec + d.coef_off, bcarry + d.coef_off / 64}, base);
-    if (g.j == sg.sub_count - 1 && bstart + cursor + 1 < total) {
+    if (g.j == sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;
     }
@@ -1058,10 +1081,132 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused destuff (images the planner gave no destuff chunks: ds_count == 0,
+// their destuffed stream fits the LDS window). The workgroup classifies the
+// cell's scan bytes itself, 16 per lane per 16 KB tile and the tiles in order,
+// with the rules of k_destuff_count/_write/_layout (ldt_kernels.hip;
+// ds_classify16), and compacts the kept bytes, the kSegPad zero pads and the
+// segment starts straight into the window (byte-swapped words, as the copy of
+// a destuffed stream leaves them), then lays out the segments' subsequences
+// in sh. No destuffed bytes go through memory. Returns false (workgroup-
+// uniform) for a corrupt image, with status 3 as k_destuff_layout sets it.
+// ---------------------------------------------------------------------------
+constexpr int kFuseTile = 16 * kHuffThreads;
+__device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ data, const ImgDesc &d,
+                                                    LDS_AS uint8_t *win, ImgLds &sh, int tid,
+                                                    int32_t *__restrict__ status, int img) {
+  // B0: the scan start rounded down to a word (pointer arithmetic on `data`
+  // only, so the loads stay global loads rather than flat ones, which an LDS
+  // wait would also wait for)
+  const int lead = (int)((uintptr_t)(data + d.src_off) & 3);
+  const uint32_t *W = reinterpret_cast<const uint32_t *>(data + (d.src_off - lead));
+  const int64_t L = d.src_len;
+  const int64_t span = L + lead;         // bytes from B0 to the end of the cell
+  const int64_t nwords = (span + 3) / 4; // words from B0 that touch the cell
+  const int last = d.nseg - 1;
+  if (tid == 0) sh.ds_end = 0x7FFFFFFF;
+  // lane words of the tile at cb: the 16 bytes at B0 + cb + 16 tid and one
+  // word on either side, zero outside the words touching the cell (ds_stage).
+  // The loads are unconditional (clamped indices): a conditional load would
+  // make the next tile's prefetch be waited for at once.
+  auto load = [&](int64_t cb, uint32_t wv[6]) {
+    const int64_t w0 = cb / 4 + 4 * tid - 1;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int64_t wi = w0 + i;
+      const uint32_t v = W[min(max(wi, (int64_t)0), nwords - 1)];
+      wv[i] = (wi >= 0 && wi < nwords) ? v : 0u;
+    }
+  };
+  auto put = [&](int o, uint32_t v) { win[o ^ 3] = (uint8_t)v; };
+  uint32_t wv[6], nx[6];
+  load(0, wv);
+  int K = 0, R = 0; // kept bytes and RSTn markers of the earlier tiles
+  for (int64_t cb = 0; cb < span; cb += kFuseTile) {
+    load(cb + kFuseTile, nx); // the next tile (clamped past the end)
+    const int64_t p0 = cb + 16 * tid - lead;
+    uint32_t keep, rst;
+    int le;
+    ds_classify16_ff(wv, p0, L, keep, rst, le);
+    if (le < 16) atomicMin(&sh.ds_end, (int)(p0 + le));
+    __syncthreads();
+    // the first end-of-scan marker ends the stream (it lies in this tile:
+    // an earlier one would have ended the loop)
+    const int E = sh.ds_end;
+    const bool ended = E != 0x7FFFFFFF;
+    if (ended) {
+      const int64_t c = (int64_t)E - p0;
+      const uint32_t lim = c <= 0 ? 0u : (c >= 16 ? 0xFFFFu : ((1u << c) - 1u));
+      keep &= lim;
+      rst &= lim;
+    }
+    int tot;
+    const int ex = block_excl_scan1024(__popc(keep) | (__popc(rst) << 16), sh.scan, &tot);
+    // kept byte o of segment r lands at o + kSegPad * min(r, last)
+    int r = R + (ex >> 16);
+    int o = K + (ex & 0xFFFF) + kSegPad * min(r, last);
+    if (rst == 0u) {
+      // kept byte j goes to o + (kept bytes before it)
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if ((keep >> j) & 1u) put(o + __popc(keep & ((1u << j) - 1u)), wv[(j + 4) >> 2] >> (8 * ((j + 4) & 3)));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if ((rst >> j) & 1u) {
+          if (r < last) {
+#pragma unroll
+            for (int q = 0; q < kSegPad; ++q) put(o + q, 0u);
+            o += kSegPad;
+          }
+          ++r;
+          if (r < d.nseg) sh.seg_pb[r] = o * 8;
+        }
+        if ((keep >> j) & 1u) put(o++, wv[(j + 4) >> 2] >> (8 * ((j + 4) & 3)));
+      }
+    }
+    K += tot & 0xFFFF;
+    R += tot >> 16;
+    if (ended) break;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) wv[i] = nx[i];
+  }
+  if (R != last) { // restart markers do not match the header
+    if (tid == 0) status[img] = 3;
+    return false;
+  }
+  // zero pad after the last segment; segment bit ranges and subsequences
+  const int tail = K + kSegPad * last;
+  if (tid < kSegPad) put(tail + tid, 0u);
+  if (tid == 0) sh.seg_pb[0] = 0;
+  __syncthreads(); // segment starts published
+  const int S = d.sub_bits;
+  int cnt_s = 0, pb = 0, nb = 0;
+  if (tid < d.nseg) {
+    pb = sh.seg_pb[tid];
+    const int end = tid + 1 < d.nseg ? sh.seg_pb[tid + 1] - 8 * kSegPad : 8 * tail;
+    nb = end - pb;
+    cnt_s = max(1, (nb + S - 1) / S);
+  }
+  int nsub;
+  const int first = block_excl_scan1024(cnt_s, sh.scan, &nsub);
+  if (tid < d.nseg) {
+    sh.seg_first[tid] = first;
+    sh.seg_nb[tid] = nb;
+  }
+  if (tid == 0) sh.seg_first[d.nseg] = nsub;
+  if (nsub > kHuffThreads) {
+    if (tid == 0) status[img] = 3;
+    return false;
+  }
+  return true;
+}
+
 __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
-    const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ dstuf,
-    const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
+    const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ data,
+    const uint8_t *__restrict__ dstuf, const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
     int16_t *__restrict__ coef, uint32_t *__restrict__ brec, uint32_t *__restrict__ bcarry,
     int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
   __shared__ ImgLds sh;
@@ -1074,15 +1219,18 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   LDS_AS uint8_t *tabs = (LDS_AS uint8_t *)(dyn_lds + win_bytes / 4);
   int slot_tab[6];
   const Dec dec = load_dec(d, htabs, tabs, tid, kHuffThreads, false, slot_tab);
-  for (int s = tid; s < d.nseg; s += kHuffThreads) {
+  const bool fused = d.ds_count == 0;
+  for (int s = tid; s < d.nseg && !fused; s += kHuffThreads) {
     const Segment &sg = segs[d.seg_base + s];
     sh.seg_first[s] = sg.sub_first;
     sh.seg_pb[s] = (int32_t)(sg.byte_start - d.dst_off) * 8; // window word 0 = dst_off
     sh.seg_nb[s] = (int32_t)((sg.byte_end - sg.byte_start) * 8);
   }
   if (tid == 0) {
-    const Segment &l = segs[d.seg_base + d.nseg - 1];
-    sh.seg_first[d.nseg] = l.sub_first + l.sub_count;
+    if (!fused) {
+      const Segment &l = segs[d.seg_base + d.nseg - 1];
+      sh.seg_first[d.nseg] = l.sub_first + l.sub_count;
+    }
     sh.need_lanes = 0;
     sh.need_waves = 0;
     sh.memo_hits = 0;
@@ -1090,7 +1238,19 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   const int64_t need = destuff_region_bytes(d.src_len, d.nseg) + 16;
   const bool in_lds = need <= win_bytes;
   const uint8_t *base = dstuf + d.dst_off; // 16-aligned
-  {
+  if (fused) {
+    // the planner fuses only images whose stream fits the window
+    if (!in_lds) {
+      if (tid == 0) status[img] = 3;
+      return;
+    }
+    for (int i = tid; i < dec.ns * kTabPieces; i += kHuffThreads) {
+      int dst;
+      const v4u v = *tab_piece_src(htabs, slot_tab, i, dst, dec.ns);
+      *(LDS_AS v4u *)(tabs + dst) = v;
+    }
+    if (!destuff_into_window(data, d, (LDS_AS uint8_t *)dyn_lds, sh, tid, status, img)) return;
+  } else {
     // Tables and (when it fits) the whole destuffed stream, byte-swapped, into
     // LDS, with all of a lane's 16-byte pieces in flight at once (a loop of
     // single loads waits on each one: ~13 dependent round trips per image).
@@ -1153,7 +1313,7 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
   if (attr != hipSuccess) return attr;
   const size_t lds = (size_t)p.win_bytes + huff_tab_lds(p.max_tabs);
   hipLaunchKernelGGL(k_huff_image, dim3(p.n_par), dim3(kHuffThreads), lds, s, p.descs, p.segs,
-                     p.htabs, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.brec, w.bcarry,
+                     p.htabs, w.data, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.brec, w.bcarry,
                      w.status, p.redo);
   return hipGetLastError();
 }

@@ -89,39 +89,7 @@ __device__ __forceinline__ void ds_classify(const uint32_t *s_in, const DsChunk 
                                             int &local_end) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) wv[i] = s_in[ds_skew(4 * tid + i)];
-  const int64_t p0 = k.cb + 16 * tid - k.lead;
-  keep = rst = 0;
-  local_end = 16;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int64_t p = p0 + j;
-    const uint32_t prev = (wv[(j + 3) >> 2] >> (8 * ((j + 3) & 3))) & 255;
-    const uint32_t cur = (wv[(j + 4) >> 2] >> (8 * ((j + 4) & 3))) & 255;
-    const uint32_t next = (wv[(j + 5) >> 2] >> (8 * ((j + 5) & 3))) & 255;
-    const bool in = p >= 0 && p < L;
-    const bool next_in = p + 1 < L;
-    bool drop = false;
-    if (cur == 0xFF) {
-      const uint32_t nx = next_in ? next : 0u;
-      if (nx == 0x00) {
-        drop = false;                        // stuffed data byte 0xFF
-      } else if (nx == 0xFF || (nx >= 0xD0 && nx <= 0xD7)) {
-        drop = true;                         // fill byte or RSTn prefix
-      } else if (in && next_in) {
-        if (local_end == 16) local_end = j;  // end-of-scan marker
-        drop = true;
-      } else {
-        drop = true;                         // trailing 0xFF at end of cell
-      }
-    } else if (prev == 0xFF && p > 0) {
-      if (cur == 0x00) drop = true;          // stuffing zero
-      else if (cur >= 0xD0 && cur <= 0xD7) {
-        drop = true;
-        if (in) rst |= 1u << j;              // RSTn code: segment boundary
-      }
-    }
-    if (in && !drop) keep |= 1u << j;
-  }
+  ds_classify16(wv, k.cb + 16 * tid - k.lead, L, keep, rst, local_end);
 }
 
 // Limit the lane's masks to bytes before the chunk's end marker (sh_end).
@@ -285,7 +253,8 @@ __global__ void __launch_bounds__(256) k_destuff_layout(const ImgDesc *__restric
   __shared__ int sh_endc;
   const int img = blockIdx.x, tid = threadIdx.x;
   const ImgDesc &d = descs[img];
-  if (status[img] != 0 || d.nseg == 0) return; // nseg 0: progressive (k_prog)
+  // nseg 0: progressive (k_prog); ds_count 0: destuffed by k_huff_image
+  if (status[img] != 0 || d.nseg == 0 || d.ds_count == 0) return;
   // chunks up to and including the first one holding the end-of-scan marker
   if (tid == 0) sh_endc = d.ds_count;
   __syncthreads();
@@ -891,8 +860,9 @@ hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s) {
     hipLaunchKernelGGL(k_destuff_write, dim3(p.n_chunks), dim3(256), 0, s, w.data, p.descs, p.segs,
                        p.chunk_img, w.ds_cnt, w.dstuf, w.status);
   }
-  hipLaunchKernelGGL(k_destuff_layout, dim3(p.n), dim3(256), 0, s, p.descs, p.segs, w.ds_cnt,
-                     w.dstuf, w.status);
+  if (p.n_ds_img > 0)
+    hipLaunchKernelGGL(k_destuff_layout, dim3(p.n), dim3(256), 0, s, p.descs, p.segs, w.ds_cnt,
+                       w.dstuf, w.status);
   return hipGetLastError();
 }
 

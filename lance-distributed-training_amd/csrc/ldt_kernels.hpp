@@ -47,6 +47,7 @@ struct DevPlan {
   const ProgTab *ptabs;
   // destuff chunks (4 KB of entropy-coded bytes each)
   int n_chunks;
+  int n_ds_img;           // baseline images destuffed by k_destuff_* (the others: k_huff_image)
   const int32_t *chunk_img; // chunk -> image
 };
 

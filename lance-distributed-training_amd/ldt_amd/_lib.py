@@ -46,6 +46,7 @@ OPT_SYNC_WARM = 7
 OPT_COPY_THREADS = 8
 OPT_HOST_TIMING = 9
 OPT_RESIZE_WAVES_PCT = 10
+OPT_FUSED_DESTUFF = 11
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
 HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status")

@@ -736,6 +736,65 @@ def test_corrupt_entropy_data_is_contained(kind):
 
 
 @pytest.mark.gpu
+def test_fused_destuff_matches_destuff_kernels(manifest):
+    """LDT_OPT_FUSED_DESTUFF: k_huff_image destuffing its image's scan bytes
+    into its LDS window gives the same tensors and the same row statuses as
+    the k_destuff_* kernels, bit for bit: goldens, config-shaped images,
+    restart markers up to the parallel decoder's 256 segments, stuffed 0xFF
+    bytes, truncated streams and randomly corrupted entropy data (stray
+    markers, deleted runs), each batch decoded both ways."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    ctx = _lib.get_context(torch.cuda.current_device())
+
+    def run(cells, fused):
+        ctx.set_option(_lib.OPT_FUSED_DESTUFF, fused)
+        try:
+            return ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy(), {}
+        except ldt_amd.ImageDecodeError as e:
+            return None, dict(e.rows)
+
+    try:
+        cells = [read_golden(e["file"]) for e in manifest["images"]]
+        c2, _ = synth.q90_512(3, seed=41)
+        c4, _ = synth.imagenet_like(3, seed=42)
+        rst256 = synth.encode(synth.field(512, 512, 43, 6.0), quality=90, restart_marker_blocks=4)
+        rst_rows = synth.encode(synth.field(375, 500, 44, 6.0), quality=95, restart_marker_rows=1)
+        cells += c2 + c4 + [rst256, rst_rows]
+        out, st = run(cells, 1)
+        assert st == {}
+        for k, b in enumerate(cells):
+            _check(out[k], oracle.jpeg_to_tensor(b), f"fused[{k}]")
+        ref, _ = run(cells, 0)
+        assert np.array_equal(out, ref)
+        rng = np.random.default_rng(45)
+        for trial in range(16):
+            base = [c2[0], rst256, rst_rows, c4[1]][trial % 4]
+            b = bytearray(base)
+            s0 = _sos_end(base)
+            for _ in range(int(rng.integers(1, 6))):
+                p = int(rng.integers(s0, len(b) - 2))
+                m = int(rng.integers(0, 3))
+                if m == 0:
+                    b[p:p + 2] = bytes([0xFF, int(rng.choice([0x00, 0xD0, 0xD5, 0xD9, 0xC4, 0xFF]))])
+                elif m == 1:
+                    b[p] ^= 1 << int(rng.integers(0, 8))
+                else:
+                    del b[p:p + int(rng.integers(1, 64))]
+            batch = [c4[0], bytes(b), bytes(base[: len(base) // 2]), c2[1]]
+            got = run(batch, 1)
+            exp = run(batch, 0)
+            assert got[1] == exp[1], (trial, got[1], exp[1])
+            if got[0] is not None:
+                assert np.array_equal(got[0], exp[0]), trial
+    finally:
+        ctx.set_option(_lib.OPT_FUSED_DESTUFF, 1)
+
+
+@pytest.mark.gpu
 def test_status_tickets_hold_two_calls():
     """ldt_last_ticket / ldt_fetch_status_ticket: a context keeps the device
     status of its last two decode calls; a batch's errors are read by ticket

@@ -141,3 +141,26 @@ def test_image_decode_error_survives_dataloader_reraise():
         w = ExceptionWrapper(where="in pin memory thread for device 0")
     with pytest.raises(ImageDecodeError, match="row 1"):
         w.reraise()
+
+
+def test_fused_destuff_classification_matches_per_byte_rules(tmp_path):
+    """The fused destuff's 0xFF-driven classification (ldt_device.hpp
+    ds_classify16_ff, used by k_huff_image) equals the per-byte rules of the
+    k_destuff_* kernels (ds_classify16) on 2M random marker-heavy cases:
+    compiled as host code with hipcc, no GPU needed."""
+    import os
+    import shutil
+    import subprocess
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "ds_classify_check"
+    subprocess.run([hipcc, "-O2", "-std=c++17", "-w",
+                    "-I", os.path.join(root, "lance-distributed-training_amd", "csrc"),
+                    os.path.join(root, "tools", "checks", "ds_classify_check.cpp"), "-o", str(exe)],
+                   check=True, timeout=300)
+    r = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout

@@ -8,7 +8,7 @@ T=$1; F=$2; shift 2
 O=$R/gpurun_out/$T
 mkdir -p $O
 cd $R
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for v in cur "$@"; do
     if [ $v = cur ]; then unset LDT_LIBRARY; else export LDT_LIBRARY=$R/lance-distributed-training_amd/ldt_amd/libldt_$v.so; fi
     timeout -k 10 300 python bench.py --no-cpu-baseline --dataset-batches 0 $F > $O/${v}_$rep.json 2> $O/${v}_$rep.err || { tail -20 $O/${v}_$rep.err; exit 1; }
