@@ -389,9 +389,7 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
   uint32_t dcd = 0;                  // its DC difference (16 bits)
   bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   while (go) {
-#ifndef LDT_EXP_OLDREFILL
     R.refill();
-#endif
     const bool first = st.k == 0; // a block starts: its DC symbol
     const uint32_t pk = R.peek();
     const uint32_t e = lookup(dec, st, pk);
@@ -441,11 +439,7 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     const uint64_t x = cg >= 0 ? (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3)) : 0ull;
     lo |= (slot & 4) ? 0ull : x;
     hi |= (slot & 4) ? x : 0ull;
-#ifndef LDT_EXP_OLDREFILL
     R.consume_nl((int)(e & 31));
-#else
-    R.consume((int)(e & 31));
-#endif
     advance(st, dec, adv);
     go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   }
