@@ -1087,11 +1087,9 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
 // uniform) for a corrupt image, with status 3 as k_destuff_layout sets it.
 // ---------------------------------------------------------------------------
 constexpr int kFuseTile = 16 * kHuffThreads;
-template <class Pre>
 __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ data, const ImgDesc &d,
                                                     LDS_AS uint8_t *win, ImgLds &sh, int tid,
-                                                    int32_t *__restrict__ status, int img,
-                                                    const Pre &after_first_load) {
+                                                    int32_t *__restrict__ status, int img) {
   // B0: the scan start rounded down to a word (pointer arithmetic on `data`
   // only, so the loads stay global loads rather than flat ones, which an LDS
   // wait would also wait for)
@@ -1118,7 +1116,6 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   auto put = [&](int o, uint32_t v) { win[o ^ 3] = (uint8_t)v; };
   uint32_t wv[6], nx[6];
   load(0, wv);
-  after_first_load(); // the caller's table stores: their loads were issued first
   int K = 0, R = 0; // kept bytes and RSTn markers of the earlier tiles
   for (int64_t cb = 0; cb < span; cb += kFuseTile) {
     load(cb + kFuseTile, nx); // the next tile (clamped past the end)
@@ -1241,21 +1238,12 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
       if (tid == 0) status[img] = 3;
       return;
     }
-    // the tables' pieces (<= 4 per lane) all in flight before the stream's
-    // first tile, stored once that tile's loads are issued too
-    constexpr int kTabPer = (6 * kTabPieces + kHuffThreads - 1) / kHuffThreads;
-    const int npc = dec.ns * kTabPieces;
-    v4u tv[kTabPer];
-    int tdst[kTabPer];
-#pragma unroll
-    for (int q = 0; q < kTabPer; ++q)
-      tv[q] = *tab_piece_src(htabs, slot_tab, min(tid + q * kHuffThreads, npc - 1), tdst[q], dec.ns);
-    auto store_tabs = [&]() {
-#pragma unroll
-      for (int q = 0; q < kTabPer; ++q)
-        if (tid + q * kHuffThreads < npc) *(LDS_AS v4u *)(tabs + tdst[q]) = tv[q];
-    };
-    if (!destuff_into_window(data, d, (LDS_AS uint8_t *)dyn_lds, sh, tid, status, img, store_tabs)) return;
+    for (int i = tid; i < dec.ns * kTabPieces; i += kHuffThreads) {
+      int dst;
+      const v4u v = *tab_piece_src(htabs, slot_tab, i, dst, dec.ns);
+      *(LDS_AS v4u *)(tabs + dst) = v;
+    }
+    if (!destuff_into_window(data, d, (LDS_AS uint8_t *)dyn_lds, sh, tid, status, img)) return;
   } else {
     // Tables and (when it fits) the whole destuffed stream, byte-swapped, into
     // LDS, with all of a lane's 16-byte pieces in flight at once (a loop of
