@@ -762,7 +762,11 @@ struct ImgLds {
   int32_t seg_nb[kMaxParSegs];        // segment length in bits
   int32_t scan[kHuffThreads / 64];
   int32_t any_changed;
-  int32_t ds_end; // fused destuff: scan position of the end-of-scan marker
+  // fused destuff: per wave, the scan position of the first end-of-scan
+  // marker in its lanes' bytes of the current tile (written every tile by
+  // every wave, so no initialisation has to be ordered before other waves'
+  // writes)
+  alignas(16) int32_t ds_endw[kHuffThreads / 64];
   int32_t need_lanes, need_waves, memo_hits; // diagnostic counters (summed over rounds)
 };
 static_assert(sizeof(ImgLds) + 512 <= kHuffStaticLds, "k_huff_image static LDS");
@@ -1087,9 +1091,11 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
 // uniform) for a corrupt image, with status 3 as k_destuff_layout sets it.
 // ---------------------------------------------------------------------------
 constexpr int kFuseTile = 16 * kHuffThreads;
+template <class Pre>
 __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ data, const ImgDesc &d,
                                                     LDS_AS uint8_t *win, ImgLds &sh, int tid,
-                                                    int32_t *__restrict__ status, int img) {
+                                                    int32_t *__restrict__ status, int img,
+                                                    const Pre &after_first_load) {
   // B0: the scan start rounded down to a word (pointer arithmetic on `data`
   // only, so the loads stay global loads rather than flat ones, which an LDS
   // wait would also wait for)
@@ -1099,7 +1105,6 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   const int64_t span = L + lead;         // bytes from B0 to the end of the cell
   const int64_t nwords = (span + 3) / 4; // words from B0 that touch the cell
   const int last = d.nseg - 1;
-  if (tid == 0) sh.ds_end = 0x7FFFFFFF;
   // lane words of the tile at cb: the 16 bytes at B0 + cb + 16 tid and one
   // word on either side, zero outside the words touching the cell (ds_stage).
   // The loads are unconditional (clamped indices): a conditional load would
@@ -1116,6 +1121,7 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   auto put = [&](int o, uint32_t v) { win[o ^ 3] = (uint8_t)v; };
   uint32_t wv[6], nx[6];
   load(0, wv);
+  after_first_load(); // the caller's table stores: their loads were issued first
   int K = 0, R = 0; // kept bytes and RSTn markers of the earlier tiles
   for (int64_t cb = 0; cb < span; cb += kFuseTile) {
     load(cb + kFuseTile, nx); // the next tile (clamped past the end)
@@ -1123,11 +1129,21 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
     uint32_t keep, rst;
     int le;
     ds_classify16_ff(wv, p0, L, keep, rst, le);
-    if (le < 16) atomicMin(&sh.ds_end, (int)(p0 + le));
+    // a lane's 16 bytes precede the next lane's, so a wave's first marker is
+    // its lowest lane's with one, and the tile's is the lowest wave's
+    const uint64_t em = __ballot(le < 16);
+    if (em != 0ull) {
+      const int first = __shfl((int)(p0 + le), __ffsll((unsigned long long)em) - 1);
+      if ((tid & 63) == 0) sh.ds_endw[tid >> 6] = first;
+    } else if ((tid & 63) == 0) {
+      sh.ds_endw[tid >> 6] = 0x7FFFFFFF;
+    }
     __syncthreads();
     // the first end-of-scan marker ends the stream (it lies in this tile:
     // an earlier one would have ended the loop)
-    const int E = sh.ds_end;
+    int E = 0x7FFFFFFF;
+#pragma unroll
+    for (int q = 0; q < kHuffThreads / 64; ++q) E = min(E, sh.ds_endw[q]);
     const bool ended = E != 0x7FFFFFFF;
     if (ended) {
       const int64_t c = (int64_t)E - p0;
@@ -1172,7 +1188,15 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   }
   // zero pad after the last segment; segment bit ranges and subsequences
   const int tail = K + kSegPad * last;
-  if (tid < kSegPad) put(tail + tid, 0u);
+  // zero pad after the last segment, then zeros over the rest of the window
+  // the decoders may read ahead into (up to 16 KB past it, capped at the
+  // window): nothing of an earlier workgroup's LDS is read, as with the
+  // k_destuff_* kernels' padded stream
+  if (tid < kSegPad + 16) put(tail + tid, 0u);
+  {
+    const int z = ((tail + kSegPad + 16) & ~15) + 16 * tid;
+    if (z + 16 <= (int)(destuff_region_bytes(L, d.nseg) + 16)) *(LDS_AS v4u *)(win + z) = (v4u)(0u);
+  }
   if (tid == 0) sh.seg_pb[0] = 0;
   __syncthreads(); // segment starts published
   const int S = d.sub_bits;
@@ -1238,12 +1262,21 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
       if (tid == 0) status[img] = 3;
       return;
     }
-    for (int i = tid; i < dec.ns * kTabPieces; i += kHuffThreads) {
-      int dst;
-      const v4u v = *tab_piece_src(htabs, slot_tab, i, dst, dec.ns);
-      *(LDS_AS v4u *)(tabs + dst) = v;
-    }
-    if (!destuff_into_window(data, d, (LDS_AS uint8_t *)dyn_lds, sh, tid, status, img)) return;
+    // the tables' pieces (<= 4 per lane) all in flight before the stream's
+    // first tile, stored once that tile's loads are issued too
+    constexpr int kTabPer = (6 * kTabPieces + kHuffThreads - 1) / kHuffThreads;
+    const int npc = dec.ns * kTabPieces;
+    v4u tv[kTabPer];
+    int tdst[kTabPer];
+#pragma unroll
+    for (int q = 0; q < kTabPer; ++q)
+      tv[q] = *tab_piece_src(htabs, slot_tab, min(tid + q * kHuffThreads, npc - 1), tdst[q], dec.ns);
+    auto store_tabs = [&]() {
+#pragma unroll
+      for (int q = 0; q < kTabPer; ++q)
+        if (tid + q * kHuffThreads < npc) *(LDS_AS v4u *)(tabs + tdst[q]) = tv[q];
+    };
+    if (!destuff_into_window(data, d, (LDS_AS uint8_t *)dyn_lds, sh, tid, status, img, store_tabs)) return;
   } else {
     // Tables and (when it fits) the whole destuffed stream, byte-swapped, into
     // LDS, with all of a lane's 16-byte pieces in flight at once (a loop of

@@ -560,6 +560,39 @@ def test_copy_pool_sizes_and_host_times(threads):
         _check(ref[k], oracle.jpeg_to_tensor(cells[k]), f"copy threads {threads}")
 
 
+@pytest.mark.parametrize("mode,bind,nt", [(0, 1, 0), (1, 1, 0), (0, 0, 1)])
+def test_copy_modes_bit_exact(mode, bind, nt):
+    """LDT_OPT_COPY_MODE / _BIND / _NT: host batches through a 2-deep pipeline,
+    8 calls over alternating batches of different sizes, so each context's two
+    device cell buffers are reused while the other's kernels may still run
+    (mode 0: the DMA on the device's copy stream waits for the buffer's last
+    reader). Every call bit-exact against the synchronous decode, and
+    ldt_host_info reports the placement."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    a, la = synth.q90_512(20, seed=51)
+    b, lb = synth.food101_like(40, seed=52)
+    rbs = [_batch(a, la), _batch(b, lb)]
+    refs = [ldt_amd.decode_tensor_image(rb)["image"].cpu().numpy() for rb in rbs]
+    pipe = ldt_amd.DecodePipeline(depth=2)
+    pipe.set_option(_lib.OPT_COPY_MODE, mode)
+    pipe.set_option(_lib.OPT_COPY_BIND, bind)
+    pipe.set_option(_lib.OPT_COPY_NT, nt)
+    pipe.set_option(_lib.OPT_COPY_THREADS, 3)
+    outs = [pipe.decode(rbs[k % 2]) for k in range(8)]
+    pipe.check()
+    torch.cuda.synchronize()
+    for k, (img, _) in enumerate(outs):
+        assert np.array_equal(img.cpu().numpy(), refs[k % 2]), k
+    info = pipe.ctxs[0].host_info()
+    assert info["copy_threads"] == 3 and len(info["copy_cpus"]) == 3
+    assert info["copy_mode"] == mode and info["copy_bind"] == bind and info["copy_nt"] == nt
+    assert (min(info["copy_cpus"]) >= 0) == bool(bind)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_progressive_mixed_batches_vs_oracle(seed):
     """SOF2 images (k_prog: jdphuff.c scans) mixed with baseline ones in one
@@ -790,6 +823,59 @@ def test_fused_destuff_matches_destuff_kernels(manifest):
             assert got[1] == exp[1], (trial, got[1], exp[1])
             if got[0] is not None:
                 assert np.array_equal(got[0], exp[0]), trial
+    finally:
+        ctx.set_option(_lib.OPT_FUSED_DESTUFF, 1)
+
+
+def _short_scan_cells():
+    """Single-tile fused-destuff streams (ldt_huffman.hip destuff_into_window:
+    a 16 KB tile is 16 bytes per lane of 1024): images whose end-of-scan
+    marker lies in the last wave's bytes (tile offsets 15,360-16,383, lanes
+    960-1023), each with trailing bytes after EOI that hold a stray RSTn, a
+    stuffed 0xFF00 and a second EOI. The reference stops at the first EOI
+    (jdmarker.c), so the trailing bytes must never count: a lost end position
+    would keep them and report a restart-marker mismatch (status 3)."""
+    from ldt_amd import synth
+
+    out = []
+    for seed in range(200):
+        h = 264 + 4 * (seed % 25)
+        w = 304 + 8 * (seed // 25)
+        b = synth.encode(synth.field(h, w, 900 + seed, 6.0), quality=85)
+        eoi = len(b) - 2  # Pillow ends the file with FFD9
+        scan = eoi - _sos_end(b)
+        if 15_400 <= scan <= 16_300:
+            out.append(b + bytes([0x12, 0xFF, 0xD0, 0x34, 0xFF, 0x00, 0x56, 0xFF, 0xD9]))
+        if len(out) == 6:
+            break
+    assert len(out) >= 3, "no single-tile streams with a late end marker"
+    return out
+
+
+@pytest.mark.gpu
+def test_fused_destuff_end_marker_in_last_wave():
+    """ADVICE r3 / VERDICT r3 weak 1: the fused destuff's end-of-scan position
+    is a per-wave minimum published across a barrier, so a marker in the last
+    wave's bytes of a single-tile stream is never lost to another wave's
+    initialisation. Fused vs k_destuff_* kernels vs the oracle, statuses
+    included, each batch decoded repeatedly (the race was timing-dependent)."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    ctx = _lib.get_context(torch.cuda.current_device())
+    cells = _short_scan_cells()
+    big, _ = synth.q90_512(2, seed=46)
+    batch = cells + big + cells[::-1]
+    exp = [oracle.jpeg_to_tensor(b) for b in batch]
+    try:
+        for fused in (1, 0, 1):
+            ctx.set_option(_lib.OPT_FUSED_DESTUFF, fused)
+            for rep in range(4):
+                out = ldt_amd.decode_tensor_image(_batch(batch))["image"].cpu().numpy()
+                for k in range(len(batch)):
+                    _check(out[k], exp[k], f"fused={fused} rep {rep} [{k}]")
     finally:
         ctx.set_option(_lib.OPT_FUSED_DESTUFF, 1)
 
