@@ -213,6 +213,11 @@ def main():
                     help="skip the configs[2]/configs[3] dataset legs (c3, c4) of a c2 run")
     ap.add_argument("--no-registered", action="store_true",
                     help="skip the host leg with the cell buffers page-locked in place (ldt_register_host)")
+    ap.add_argument("--host-depth", type=int, default=2,
+                    help="batches in flight of the host-input legs (make_to_tensor_fn(depth)): with the cells' "
+                         "copy stream, depth + 2 streams fit the process's 4 hardware queues at depth 2")
+    ap.add_argument("--host-reps", type=int, default=3,
+                    help="back-to-back runs of the copying host-input leg (value_host_input = their median)")
     ap.add_argument("--dataset-copy", action="store_true",
                     help="dataset legs through the copying to_tensor_fn instead of registering the mapped "
                          "fragments' image buffers")
@@ -244,6 +249,12 @@ def main():
     wl = WORKLOADS[args.workload]
     B = args.batch or wl["batch"]
     ctx = _lib.get_context(dev.index)
+    numa_cpus = None
+    if os.environ.get("LDT_BENCH_NUMA", "1") != "0":
+        # this rank on its GPU's NUMA node (numactl --cpunodebind per rank):
+        # the host batches below are then allocated there, where the copy
+        # pool reads them
+        numa_cpus = len(ldt_amd.bind_numa(dev))
     ctx.set_option(_lib.OPT_SYNC_STATUS, 0)
     ctx.set_option(_lib.OPT_PROFILE, 0 if args.no_stage_events else 1)
 
@@ -320,7 +331,7 @@ def main():
     # the plug-in boundary: the same steps with the cells in
     # host Arrow RecordBatches through the pipelined to_tensor_fn
     def host_rate(bs, register=False):
-        fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev, register=register)
+        fn = ldt_amd.make_to_tensor_fn(depth=args.host_depth, device=dev, register=register)
         fn.pipeline.set_option(_lib.OPT_HOST_TIMING, 1)
         fn.pipeline.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
         k = [0]
@@ -336,18 +347,38 @@ def main():
         t = timed(hstep, args.steps, 0)
         fn.check()
         us, calls = fn.pipeline.host_times(reset=True)
+        info = fn.pipeline.ctxs[0].host_info()
         if register:
             fn.release()
-        return B * args.steps * world / t, {k_: round(v / max(calls, 1), 1) for k_, v in us.items()}
+        return B * args.steps * world / t, {k_: round(v / max(calls, 1), 1) for k_, v in us.items()}, info
 
-    value_host = value_registered = host_us = None
+    value_host = value_registered = host_us = host_info = None
+    host_reps = []
     if args.workload != "c5":
-        value_host, host_us = host_rate(host_batches)
+        # the copying leg (the plug-in contract: fresh host batches every call)
+        # `host_reps` times back to back; value_host_input = the median
+        for _ in range(max(1, args.host_reps)):
+            v, host_us, host_info = host_rate(host_batches)
+            host_reps.append(v)
+        value_host = sorted(host_reps)[len(host_reps) // 2]
         if not args.no_registered:
             try:
-                value_registered, _ = host_rate(host_batches, register=True)
+                value_registered, _, _ = host_rate(host_batches, register=True)
             except ldt_amd.LdtError as e:
                 print(f"bench: registered host leg skipped: {e}", file=sys.stderr)
+    # every rank's host copy placement and host phases (the node's host budget:
+    # copy threads per rank from the cgroup quota / LOCAL_WORLD_SIZE, cores on
+    # the rank's GPU-local NUMA node)
+    host_ranks = None
+    if host_info is not None:
+        mine = {"rank": rank, "local_rank": local, "device": dev.index, "host_us_per_call": host_us,
+                **{k_: host_info[k_] for k_ in ("copy_threads", "copy_cpus", "gpu_numa", "quota_cpus",
+                                                 "local_world")}}
+        if world > 1:
+            host_ranks = [None] * world
+            dist.all_gather_object(host_ranks, mine)
+        else:
+            host_ranks = [mine]
 
     value_dataset = None
     dataset_info = None
@@ -439,10 +470,14 @@ def main():
         res["value_host_input_per_gpu"] = round(value_host / world, 1)
         res["value_host_input_note"] = ("the same steps with the cells in host pa.RecordBatches through the "
                                         "pipelined to_tensor_fn (make_to_tensor_fn(depth)): pinned copy "
-                                        "overlapped with the header walk + H2D every step; "
+                                        "overlapped with the header walk, one H2D DMA per step on the "
+                                        "device's copy stream; median of value_host_input_reps; "
                                         "value_host_registered: the same with the two batches' image buffers "
                                         "page-locked in place (register=True), DMA without the host copy")
         res["host_us_per_call"] = host_us
+        res["value_host_input_reps"] = [round(v, 1) for v in host_reps]
+        res["host_placement"] = dict(host_info, numa_bound_cpus=numa_cpus, host_depth=args.host_depth)
+        res["host_ranks"] = host_ranks
     if value_registered is not None:
         res["value_host_registered"] = round(value_registered, 1)
     if config_legs:

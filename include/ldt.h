@@ -77,7 +77,8 @@ extern "C" {
 #define LDT_OPT_COPY_THREADS 8 /* threads of the context's host copy pool that
                                  move a batch's cells into the pinned slot while
                                  the calling thread walks the headers (0..31;
-                                 -1 = default, min(6, cores - 2))             */
+                                 -1 = default: the cgroup CPU quota divided by
+                                 LOCAL_WORLD_SIZE, minus 2, at most 6)         */
 #define LDT_OPT_HOST_TIMING 9 /* 1: accumulate host phase times of every
                                  decode call (read with ldt_host_times)        */
 #define LDT_OPT_RESIZE_WAVES_PCT 10 /* resize bands per batch as % of one full
@@ -89,6 +90,17 @@ extern "C" {
                                  stream fits its LDS window itself; 0: every
                                  image through the k_destuff_* kernels
                                  (cross-check)                                  */
+#define LDT_OPT_COPY_MODE 12  /* 0 (default): a host batch's cells go to HBM in
+                                 one DMA on a per-device copy stream, which
+                                 `stream` waits for (the transfer overlaps the
+                                 kernels of earlier batches); 1: the DMA on
+                                 `stream` itself                              */
+#define LDT_OPT_COPY_BIND 13  /* 1 (default): copy-pool threads bound to
+                                 physical cores local to the GPU's NUMA node,
+                                 spread over its L3 domains, the block of
+                                 cores chosen by LOCAL_RANK; 0: unbound         */
+#define LDT_OPT_COPY_NT 14    /* 1 (default): the copy pool writes the pinned slot with
+                                 non-temporal stores (AVX2, default); 0: memcpy */
 
 /* ---- stages reported by ldt_stage_times ---- */
 #define LDT_STAGE_H2D 0       /* cell + plan copies into HBM                   */
@@ -188,9 +200,20 @@ int ldt_stage_times(ldt_ctx *ctx, double *ms_out, int64_t *count_out, int reset)
 /* Host phase times (LDT_OPT_HOST_TIMING = 1), microseconds summed over the
  * timed calls since the last reset, into us_out[LDT_NUM_HOST_PHASES]:
  * pinned slot + copy start, header walk (overlaps the cell copy), plan blob,
- * cell copy join + H2D enqueue, kernel launches, status; *calls_out = calls. */
-#define LDT_NUM_HOST_PHASES 6
+ * cell copy join + H2D enqueue, kernel launches, status; then two copy-pool
+ * diagnostics that overlap those: the pool's wake-up (copy start to the first
+ * chunk a pool thread took) and the copy's span (start to last chunk done);
+ * *calls_out = calls. */
+#define LDT_NUM_HOST_PHASES 8
 int ldt_host_times(ldt_ctx *ctx, double *us_out, int64_t *calls_out, int reset);
+
+/* The context's host copy placement as a JSON object (NUL-terminated, into
+ * buf[len]): copy_threads, copy_cpus, gpu_numa (the GPU's NUMA node from
+ * sysfs), quota_cpus (cgroup), local_rank / local_world (torchrun's
+ * LOCAL_RANK / LOCAL_WORLD_SIZE), l3_domains, candidate_cores, and the
+ * copy_bind / copy_nt / copy_mode options, local_cpulist (the GPU's local
+ * CPUs from sysfs, "" if unknown). Creates the pool if needed. */
+int ldt_host_info(ldt_ctx *ctx, char *buf, size_t len);
 
 /* Config 5: raw uint8 HWC cells (no JPEG) -> Resize(224,224) [+Normalize] ->
  * float32 [n,3,224,224]. `hwc` is a device pointer when hwc_is_device != 0,

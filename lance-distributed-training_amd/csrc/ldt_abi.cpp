@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/ldt.h"
+#include "ldt_hostcopy.hpp"
 #include "ldt_kernels.hpp"
 #include "ldt_plan.hpp"
 
@@ -54,132 +55,6 @@ struct PinBuf {
   size_t cap = 0;
 };
 
-// Host copies into the pinned ring (Arrow cells -> pinned -> HBM) are the
-// host-side bottleneck of the PCIe path: one core moves ~6-10 GB/s. A small
-// persistent pool per context copies a batch's cells in chunks while the
-// calling thread walks the JPEG headers (decode_core): start() hands the copy
-// to the pool and returns, finish() joins in on the chunks still untaken and
-// waits for the rest. Chunks are claimed with one 64-bit ticket (generation in
-// the high half), so a thread still looping over an old copy can never take a
-// chunk of the next one.
-class CopyPool {
-public:
-  // device: the HIP device the chunk DMAs are enqueued for (each pool thread
-  // selects it once)
-  CopyPool(int nthreads, int device) {
-    for (int i = 0; i < nthreads; ++i)
-      th_.emplace_back([this, device] {
-        (void)hipSetDevice(device);
-        run();
-      });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-      ++gen_;
-    }
-    cv_.notify_all();
-    for (auto &t : th_) t.join();
-  }
-  int threads() const { return (int)th_.size(); }
-  // Copy n bytes src -> dst (pinned). With dev_dst, every chunk is also
-  // enqueued as an H2D DMA dst -> dev_dst on `stream` as soon as its memcpy is
-  // done, so the PCIe transfer runs behind the host copy instead of after it;
-  // finish() returns once every chunk is copied and its DMA enqueued (all of
-  // them before anything the caller enqueues on `stream` afterwards).
-  void start(void *dst, const void *src, size_t n, void *dev_dst = nullptr, hipStream_t stream = nullptr) {
-    dma_err_ = hipSuccess;
-    if (th_.empty() || n < ((size_t)1 << 20)) {
-      memcpy(dst, src, n);
-      if (dev_dst) dma_err_ = hipMemcpyAsync(dev_dst, dst, n, hipMemcpyHostToDevice, stream);
-      sync_done_ = true;
-      return;
-    }
-    sync_done_ = false;
-    {
-      std::lock_guard<std::mutex> g(m_);
-      dst_ = static_cast<uint8_t *>(dst);
-      src_ = static_cast<const uint8_t *>(src);
-      dev_ = static_cast<uint8_t *>(dev_dst);
-      stream_ = stream;
-      n_ = n;
-      // ~4 chunks per thread (the caller joins late), at least 256 KB; with
-      // DMA, at least 1 MB so that a transfer is not dominated by its setup
-      const size_t parts = 4 * (th_.size() + 1);
-      const size_t minc = dev_dst ? (size_t)1 << 20 : (size_t)1 << 18;
-      chunk_ = std::max<size_t>(((n + parts - 1) / parts + 4095) & ~(size_t)4095, minc);
-      nchunks_ = (uint32_t)((n + chunk_ - 1) / chunk_);
-      done_ = 0;
-      ++gen_;
-      ticket_.store((uint64_t)(uint32_t)gen_ << 32, std::memory_order_release);
-    }
-    cv_.notify_all();
-  }
-  // Take part in the copy until no chunk is left, then wait for all of them.
-  // Returns the first failed DMA enqueue (hipSuccess if none).
-  hipError_t finish() {
-    if (sync_done_) return dma_err_;
-    uint32_t g;
-    {
-      std::lock_guard<std::mutex> l(m_);
-      g = (uint32_t)gen_;
-    }
-    work(g);
-    std::unique_lock<std::mutex> lk(m_);
-    done_cv_.wait(lk, [this] { return done_ == nchunks_; });
-    sync_done_ = true;
-    return dma_err_;
-  }
-
-private:
-  void work(uint32_t g) {
-    for (;;) {
-      // claim chunk i of generation g only (a fetch_add could consume a
-      // chunk of a newer copy that this thread then would not do)
-      uint64_t t = ticket_.load(std::memory_order_acquire);
-      do {
-        if ((uint32_t)(t >> 32) != g || (uint32_t)t >= nchunks_) return;
-      } while (!ticket_.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel,
-                                              std::memory_order_acquire));
-      const uint32_t i = (uint32_t)t;
-      const size_t lo = (size_t)i * chunk_, hi = std::min(n_, lo + chunk_);
-      memcpy(dst_ + lo, src_ + lo, hi - lo);
-      hipError_t e = hipSuccess;
-      if (dev_) e = hipMemcpyAsync(dev_ + lo, dst_ + lo, hi - lo, hipMemcpyHostToDevice, stream_);
-      std::lock_guard<std::mutex> l(m_);
-      if (e != hipSuccess && dma_err_ == hipSuccess) dma_err_ = e;
-      if (++done_ == nchunks_) done_cv_.notify_all();
-    }
-  }
-  void run() {
-    uint64_t seen = 0;
-    for (;;) {
-      uint32_t g;
-      {
-        std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (stop_) return;
-        g = (uint32_t)gen_;
-      }
-      work(g);
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex m_;
-  std::condition_variable cv_, done_cv_;
-  uint64_t gen_ = 0;
-  std::atomic<uint64_t> ticket_{0};
-  bool stop_ = false, sync_done_ = true;
-  uint8_t *dst_ = nullptr, *dev_ = nullptr;
-  const uint8_t *src_ = nullptr;
-  hipStream_t stream_ = nullptr;
-  size_t n_ = 0, chunk_ = 0;
-  uint32_t nchunks_ = 0, done_ = 0;
-  hipError_t dma_err_ = hipSuccess;
-};
-
 // Host phases of decode_core (LDT_OPT_HOST_TIMING; read with ldt_host_times).
 enum HostPhase {
   kHpSlot = 0, // waiting for the pinned slot, starting the cell copy
@@ -188,6 +63,10 @@ enum HostPhase {
   kHpCopy,     // waiting for the cell copy to finish, H2D enqueue
   kHpLaunch,   // kernel launches
   kHpStatus,   // status copy, return
+  // not phases of the calling thread: the copy pool's wake-up (copy start to
+  // the first chunk a pool thread took) and span (copy start to its end)
+  kHpCopyWake,
+  kHpCopySpan,
   kHpCount
 };
 
@@ -205,12 +84,22 @@ struct ldt_ctx {
   int subseq_bits = 256; // minimum S of the parallel decoder
   int resize_waves_pct = 100;
   bool fuse_destuff = LDT_FUSE_DEFAULT; // LDT_OPT_FUSED_DESTUFF
-  int copy_threads = -1; // -1: default (min(6, cores - 2))
+  int copy_threads = -1; // -1: default (from the cgroup quota per local rank, <= 6)
+  bool copy_bind = true;  // LDT_OPT_COPY_BIND: pool threads on GPU-local cores
+  bool copy_nt = true;    // LDT_OPT_COPY_NT: non-temporal stores into the slot
+  int copy_mode = 0;      // LDT_OPT_COPY_MODE: 0 DMA on the device's copy stream, 1 on the caller's
   bool host_timing = false;
-  DevBuf d_data, d_plan, d_dstuf, d_coef, d_brec, d_bcarry, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt;
+  CopyPlacement placement; // of the current pool
+  static constexpr int kSlots = 2;
+  // device cells, one buffer per pinned slot: a copy-stream DMA into one may
+  // run while the kernels of the slot's previous batch still read the other
+  DevBuf d_data[kSlots];
+  hipEvent_t data_free_ev[kSlots] = {nullptr, nullptr}; // its last reader (Huffman stage) done
+  hipEvent_t h2d_ev[kSlots] = {nullptr, nullptr};       // its DMA done (copy stream)
+  bool data_used[kSlots] = {false, false};
+  DevBuf d_plan, d_dstuf, d_coef, d_brec, d_bcarry, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt;
   DevBuf d_perm; // DistributedSampler scratch: 3 int32 arrays of dataset_len
   std::unique_ptr<CopyPool> copier; // host -> pinned copies (created on first use)
-  static constexpr int kSlots = 2;
   PinBuf h_data[kSlots], h_plan[kSlots];
   hipEvent_t slot_ev[kSlots] = {nullptr, nullptr};
   bool slot_used[kSlots] = {false, false};
@@ -247,7 +136,7 @@ struct ldt_ctx {
   int64_t stage_cnt[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
   EvSet *cur_ev = nullptr;
   int64_t last_off_redo = -1; // debug counters of the last batch (plan blob offset)
-  double host_us[kHpCount] = {0, 0, 0, 0, 0, 0};
+  double host_us[kHpCount] = {};
   int64_t host_calls = 0;
 };
 
@@ -366,16 +255,13 @@ bool host_registered(const void *p, size_t n) {
 
 CopyPool &copier(ldt_ctx *c) {
   if (!c->copier) {
-    int nt = c->copy_threads;
-    if (nt < 0) {
-      // the CPUs this process may run on (hardware_concurrency counts the
-      // whole host); ~7 copying threads with the caller saturate PCIe
-      cpu_set_t cs;
-      int cpus = (int)std::thread::hardware_concurrency();
-      if (sched_getaffinity(0, sizeof(cs), &cs) == 0) cpus = CPU_COUNT(&cs);
-      nt = std::min(6, std::max(0, cpus - 2));
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), c->device) != hipSuccess) {
+      (void)hipGetLastError();
+      bus[0] = 0;
     }
-    c->copier.reset(new CopyPool(std::max(0, std::min(nt, 31)), c->device));
+    c->placement = copy_placement(bus, c->copy_threads, c->copy_bind);
+    c->copier.reset(new CopyPool(c->placement.cpus, c->copy_nt));
   }
   return *c->copier;
 }
@@ -383,19 +269,34 @@ CopyPool &copier(ldt_ctx *c) {
 void pinned_copy(ldt_ctx *c, void *dst, const void *src, size_t n) {
   CopyPool &p = copier(c);
   p.start(dst, src, n);
-  (void)p.finish();
+  p.finish();
+}
+
+// One non-blocking stream per device for the cells' H2D DMA (LDT_OPT_COPY_MODE
+// 0), shared by the process's contexts: the transfer of a batch then runs
+// while the kernels of the batches before it still occupy the contexts'
+// streams (one more HIP stream per process; the copy engine does the work).
+hipStream_t copy_stream(int device) {
+  static std::mutex m;
+  static hipStream_t streams[64] = {};
+  std::lock_guard<std::mutex> l(m);
+  if (device < 0 || device >= 64) return nullptr;
+  if (!streams[device] && hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    streams[device] = nullptr;
+  }
+  return streams[device];
 }
 
 // Joins an asynchronous cell copy on every exit path of decode_core: the
 // caller's host buffer is borrowed only for the duration of the call.
 struct CopyJoin {
   CopyPool *p = nullptr;
-  hipError_t wait() {
-    hipError_t e = p ? p->finish() : hipSuccess;
+  void wait() {
+    if (p) p->finish();
     p = nullptr;
-    return e;
   }
-  ~CopyJoin() { (void)wait(); }
+  ~CopyJoin() { wait(); }
 };
 
 int ensure_pin(ldt_ctx *c, PinBuf &b, size_t need) {
@@ -486,6 +387,23 @@ void build_lut(const ldt_norm *norm, float *lut) {
     }
 }
 
+// The batch's cells (pinned slot or registered pages) -> the slot's device
+// buffer. LDT_OPT_COPY_MODE 0: one DMA on the device's copy stream, after the
+// kernels that last read that buffer; `s` waits for it. Mode 1 (or no copy
+// stream): on `s` itself, behind the previous batch's kernels.
+int enqueue_cells(ldt_ctx *c, int sl, const void *src, size_t n, hipStream_t s) {
+  hipStream_t cs = c->copy_mode == 0 ? copy_stream(c->device) : nullptr;
+  if (!cs) {
+    HIPCHK(c, hipMemcpyAsync(c->d_data[sl].p, src, n, hipMemcpyHostToDevice, s));
+    return LDT_OK;
+  }
+  if (c->data_used[sl]) HIPCHK(c, hipStreamWaitEvent(cs, c->data_free_ev[sl], 0));
+  HIPCHK(c, hipMemcpyAsync(c->d_data[sl].p, src, n, hipMemcpyHostToDevice, cs));
+  HIPCHK(c, hipEventRecord(c->h2d_ev[sl], cs));
+  HIPCHK(c, hipStreamWaitEvent(s, c->h2d_ev[sl], 0));
+  return LDT_OK;
+}
+
 struct ImgPlan {
   Header H;
   int status = LDT_IMG_OK;
@@ -520,24 +438,23 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   }
 
   // ---- pinned slot, then the cells' way to HBM, which the header walk below
-  // overlaps: the pool threads copy them into the slot in chunks and enqueue
-  // each chunk's H2D DMA as soon as it is copied (a registered range is
-  // DMAed from the caller's pages at once). The copy is joined before the
-  // plan upload and the kernels are enqueued behind it on `s`. ----
+  // overlaps: the pool threads copy them into the slot (a registered range is
+  // DMAed from the caller's pages at once). The copy is joined after the
+  // header walk and the batch goes to HBM in one DMA (enqueue_cells). ----
   if ((rc = acquire_slot(c))) return rc;
   const int sl = c->slot;
   std::shared_ptr<HostRange> reg; // registered range the H2D reads from
   CopyJoin cj;
   prof_begin(c, LDT_STAGE_H2D, s);
   if (!data_dev && total_bytes > 0) {
-    if ((rc = ensure_dev(c, c->d_data, (size_t)total_bytes + 16, s))) return rc;
+    if ((rc = ensure_dev(c, c->d_data[sl], (size_t)total_bytes + 16, s))) return rc;
     reg = host_acquire(cells_host, (size_t)total_bytes, c->device);
     if (reg) {
-      HIPCHK(c, hipMemcpyAsync(c->d_data.p, cells_host, (size_t)total_bytes, hipMemcpyHostToDevice, s));
+      if ((rc = enqueue_cells(c, sl, cells_host, (size_t)total_bytes, s))) return rc;
     } else {
       if ((rc = ensure_pin_slots(c, c->h_data, sl, (size_t)total_bytes + 16))) return rc;
       CopyPool &pool = copier(c);
-      pool.start(c->h_data[sl].p, cells_host, (size_t)total_bytes, c->d_data.p, s);
+      pool.start(c->h_data[sl].p, cells_host, (size_t)total_bytes);
       cj.p = &pool;
     }
   }
@@ -972,10 +889,18 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   ht.mark(kHpPlan); // plan blob written, buffers sized
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
-    // every chunk copied into the slot and its DMA enqueued
-    HIPCHK(c, cj.wait());
+    if (cj.p) {
+      // every chunk copied into the slot: one DMA of the batch
+      CopyPool *pool = cj.p;
+      cj.wait();
+      if (c->host_timing) {
+        c->host_us[kHpCopyWake] += std::max(0.0, pool->last_wake_us());
+        c->host_us[kHpCopySpan] += pool->last_span_us();
+      }
+      if ((rc = enqueue_cells(c, sl, c->h_data[sl].p, (size_t)total_bytes, s))) return rc;
+    }
     host_release(reg);
-    dev_cells = static_cast<const uint8_t *>(c->d_data.p);
+    dev_cells = static_cast<const uint8_t *>(c->d_data[sl].p);
   }
   HIPCHK(c, hipMemcpyAsync(c->d_plan.p, hp, (size_t)plan_bytes, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipEventRecord(c->slot_ev[sl], s));
@@ -1040,6 +965,12 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_prog(p, w, s));
   HIPCHK(c, launch_dc_scan(p, w, s));
+  if (!data_dev) {
+    // the cells' last readers are enqueued: a later DMA into this slot's
+    // device buffer waits for them (copy stream)
+    HIPCHK(c, hipEventRecord(c->data_free_ev[sl], s));
+    c->data_used[sl] = true;
+  }
   prof_mark(c, LDT_STAGE_HUFFMAN, s);
   HIPCHK(c, launch_idct(p, w, s));
   c->coef_dirty = false;
@@ -1111,7 +1042,9 @@ ldt_ctx *ldt_create(int device, size_t max_batch_bytes, int max_n) {
   DeviceGuard g(device);
   for (int k = 0; k < ldt_ctx::kSlots; ++k)
     if (hipEventCreateWithFlags(&c->slot_ev[k], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->st_ev[k], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->st_ev[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->data_free_ev[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->h2d_ev[k], hipEventDisableTiming) != hipSuccess) {
       delete c;
       return nullptr;
     }
@@ -1120,7 +1053,7 @@ ldt_ctx *ldt_create(int device, size_t max_batch_bytes, int max_n) {
     return nullptr;
   }
   if (max_batch_bytes > 0) {
-    (void)ensure_dev(c, c->d_data, max_batch_bytes, nullptr);
+    for (int k = 0; k < ldt_ctx::kSlots; ++k) (void)ensure_dev(c, c->d_data[k], max_batch_bytes, nullptr);
     for (int k = 0; k < ldt_ctx::kSlots; ++k) (void)ensure_pin(c, c->h_data[k], max_batch_bytes);
   }
   (void)max_n;
@@ -1131,7 +1064,7 @@ void ldt_destroy(ldt_ctx *c) {
   if (!c) return;
   DeviceGuard g(c->device);
   (void)hipDeviceSynchronize();
-  DevBuf *dbs[] = {&c->d_data, &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_brec, &c->d_bcarry, &c->d_pcoef, &c->d_dcv,
+  DevBuf *dbs[] = {&c->d_data[0], &c->d_data[1], &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_brec, &c->d_bcarry, &c->d_pcoef, &c->d_dcv,
                     &c->d_planes, &c->d_raw, &c->d_dscnt};
   for (DevBuf *b : dbs)
     if (b->p) (void)hipFree(b->p);
@@ -1140,6 +1073,8 @@ void ldt_destroy(ldt_ctx *c) {
     if (c->h_plan[k].p) (void)hipHostFree(c->h_plan[k].p);
     if (c->slot_ev[k]) (void)hipEventDestroy(c->slot_ev[k]);
     if (c->st_ev[k]) (void)hipEventDestroy(c->st_ev[k]);
+    if (c->data_free_ev[k]) (void)hipEventDestroy(c->data_free_ev[k]);
+    if (c->h2d_ev[k]) (void)hipEventDestroy(c->h2d_ev[k]);
     if (c->h_status[k]) (void)hipHostFree(c->h_status[k]);
   }
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -1238,6 +1173,22 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
   case LDT_OPT_FUSED_DESTUFF:
     c->fuse_destuff = value != 0;
     return LDT_OK;
+  case LDT_OPT_COPY_MODE:
+    if (value < 0 || value > 1) return set_err(c, LDT_ERR_ARG, "copy mode %lld", (long long)value);
+    c->copy_mode = (int)value;
+    return LDT_OK;
+  case LDT_OPT_COPY_BIND:
+    if ((value != 0) != c->copy_bind) {
+      c->copy_bind = value != 0;
+      c->copier.reset();
+    }
+    return LDT_OK;
+  case LDT_OPT_COPY_NT:
+    if ((value != 0) != c->copy_nt) {
+      c->copy_nt = value != 0;
+      c->copier.reset();
+    }
+    return LDT_OK;
   default:
     return set_err(c, LDT_ERR_ARG, "unknown option %d", option);
   }
@@ -1272,6 +1223,23 @@ int ldt_decode_batch_resident(ldt_ctx *c, const uint8_t *data_host, const uint8_
   return decode_core<int64_t>(c, data_host, data_dev, offsets, 0, n, nullptr, labels, 0,
                               out_img_dev, out_lbl_dev, norm, (hipStream_t)stream,
                               per_image_status);
+}
+
+int ldt_host_info(ldt_ctx *c, char *buf, size_t len) {
+  if (!c || !buf || len == 0) return LDT_ERR_ARG;
+  DeviceGuard g(c->device);
+  (void)copier(c); // placement of the pool the next copy uses
+  const CopyPlacement &P = c->placement;
+  std::string cpus;
+  for (size_t i = 0; i < P.cpus.size(); ++i) cpus += (i ? "," : "") + std::to_string(P.cpus[i]);
+  const int w = snprintf(buf, len,
+                         "{\"copy_threads\": %d, \"copy_cpus\": [%s], \"gpu_numa\": %d, \"quota_cpus\": %.2f, "
+                         "\"local_rank\": %d, \"local_world\": %d, \"l3_domains\": %d, \"candidate_cores\": %d, "
+                         "\"copy_bind\": %d, \"copy_nt\": %d, \"copy_mode\": %d, \"local_cpulist\": \"%s\"}",
+                         (int)P.cpus.size(), cpus.c_str(), P.gpu_numa, P.quota_cpus, P.local_rank, P.local_world,
+                         P.l3_domains, P.candidates, c->copy_bind ? 1 : 0, c->copy_nt ? 1 : 0, c->copy_mode,
+                         P.local_cpulist.c_str());
+  return w >= 0 && (size_t)w < len ? LDT_OK : set_err(c, LDT_ERR_ARG, "host info: buffer of %zu bytes too small", len);
 }
 
 int ldt_host_times(ldt_ctx *c, double *us_out, int64_t *calls_out, int reset) {

@@ -14,6 +14,15 @@ import threading
 
 import torch  # noqa: F401  (must load torch's HIP runtime before libldt.so)
 
+
+def hw_queues() -> int:
+    """Hardware queues per process the HIP runtime uses (ROCclr's
+    GPU_MAX_HW_QUEUES, default 4): streams beyond it share a queue."""
+    try:
+        return int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        return 4
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libldt.so")
 
@@ -47,16 +56,19 @@ OPT_COPY_THREADS = 8
 OPT_HOST_TIMING = 9
 OPT_RESIZE_WAVES_PCT = 10
 OPT_FUSED_DESTUFF = 11
+OPT_COPY_MODE = 12
+OPT_COPY_BIND = 13
+OPT_COPY_NT = 14
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
-HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status")
+HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status", "copy_wake", "copy_span")
 
 # Every symbol include/ldt.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "ldt_create", "ldt_destroy", "ldt_last_error", "ldt_set_option", "ldt_version",
     "ldt_decode_batch", "ldt_decode_batch_large", "ldt_decode_batch_resident",
     "ldt_register_host", "ldt_unregister_host", "ldt_fetch_status", "ldt_last_ticket", "ldt_fetch_status_ticket",
-    "ldt_stage_times", "ldt_host_times", "ldt_resize_raw", "ldt_shard_ranges",
+    "ldt_stage_times", "ldt_host_times", "ldt_host_info", "ldt_resize_raw", "ldt_shard_ranges",
     "ldt_shard_fragments", "ldt_distributed_indices",
 )
 
@@ -126,6 +138,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_fetch_status_ticket.argtypes = [vp, i64, vp, i64]
         L.ldt_stage_times.argtypes = [vp, vp, vp, i32]
         L.ldt_host_times.argtypes = [vp, vp, vp, i32]
+        L.ldt_host_info.argtypes = [vp, ctypes.c_char_p, sz]
         L.ldt_resize_raw.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, vp, vp]
         L.ldt_shard_ranges.argtypes = [vp, i64, i64, i32, i32, vp, i64, vp, vp]
         L.ldt_shard_fragments.argtypes = [vp, vp, i32, i64, i32, i32, i64, vp, i64, vp, vp, vp]
@@ -137,7 +150,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_unregister_host.argtypes = [vp, vp]
         for name in ("ldt_set_option", "ldt_decode_batch", "ldt_decode_batch_large", "ldt_register_host",
                      "ldt_unregister_host",
-                     "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_fetch_status_ticket", "ldt_resize_raw", "ldt_stage_times", "ldt_host_times",
+                     "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_fetch_status_ticket", "ldt_resize_raw", "ldt_stage_times", "ldt_host_times", "ldt_host_info",
                      "ldt_shard_ranges", "ldt_shard_fragments", "ldt_distributed_indices",
                      "ldt_debug_resample_coeffs",
                      "ldt_debug_counters"):
@@ -185,6 +198,15 @@ class Context:
         self.check(self.lib.ldt_host_times(self.handle, us.ctypes.data, ctypes.byref(calls), int(reset)),
                    "ldt_host_times")
         return {k: float(us[i]) for i, k in enumerate(HOST_PHASES)}, int(calls.value)
+
+    def host_info(self) -> dict:
+        """The host copy placement (ldt_host_info): copy threads and their
+        CPUs, the GPU's NUMA node, the cgroup quota, local rank/world."""
+        import json
+
+        buf = ctypes.create_string_buffer(4096)
+        self.check(self.lib.ldt_host_info(self.handle, buf, len(buf)), "ldt_host_info")
+        return json.loads(buf.value.decode())
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -428,6 +428,37 @@ def resize_raw(hwc, height: int, width: int, *, device=None, normalize=True):
     return out
 
 
+def _parse_cpulist(s: str):
+    out = set()
+    for part in s.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def bind_numa(device=None):
+    """Restrict the calling thread (and the threads and processes it starts
+    later) to the CPUs local to `device`'s NUMA node, within its current
+    affinity — `numactl --cpunodebind` for one rank. Host buffers the thread
+    allocates afterwards (Arrow batches read in it) then land on the GPU's
+    node by first touch, so the copy pool (bound there, ldt_host_info) reads
+    them locally: from a remote node its copy runs at the inter-socket link's
+    ~48 GB/s instead of ~170 GB/s. Returns the CPUs now allowed
+    (unchanged if the GPU's local CPUs are unknown or outside the affinity)."""
+    import os
+
+    info = _decoder(device).ctx.host_info()
+    cur = os.sched_getaffinity(0)
+    local = _parse_cpulist(info.get("local_cpulist", "")) & cur
+    if local and local != cur:
+        os.sched_setaffinity(0, local)
+        return local
+    return cur
+
+
 def _host_range(obj):
     """(address, size) of the host bytes behind a pa.Buffer, the data buffer of
     a binary/large_binary/fixed_size_binary pa.Array / ChunkedArray chunk, or
@@ -542,6 +573,13 @@ class DecodePipeline:
             c.set_option(_lib.OPT_SYNC_STATUS, 0)
             if profile:
                 c.set_option(_lib.OPT_PROFILE, 1)
+        # the cells' DMA of host batches goes on the device's copy stream when
+        # the process has a hardware queue for it beside the slots' streams and
+        # the consumer's (otherwise two streams would share a queue and the
+        # slots' kernels serialise): else on the slot's own stream
+        if _lib.hw_queues() < self.depth + 2:
+            for c in self.ctxs:
+                c.set_option(_lib.OPT_COPY_MODE, 1)
         self.streams = [torch.cuda.Stream(self.dec.device) for _ in range(self.depth)]
         self.pending = [deque() for _ in range(self.depth)]  # per slot: (ticket, n), oldest first
         self.last_ticket = None  # (slot, ticket) of the most recent decode

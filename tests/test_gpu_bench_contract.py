@@ -60,27 +60,41 @@ def _free_port():
 
 
 @pytest.mark.gpu
-def test_bench_two_rank_rehearsal():
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_bench_multi_rank_rehearsal(ranks):
     """The N > 1 path of bench.py as the driver launches it (torchrun, one
     process per rank, barriers, max over ranks, rank 0 prints one line), with
-    LDT_BENCH_BACKEND=gloo so that both ranks can share this box's one GPU."""
+    LDT_BENCH_BACKEND=gloo so that the ranks can share this box's one GPU. At
+    8 ranks it rehearses the node's host budget: every rank sizes its copy
+    pool from the cgroup quota / LOCAL_WORLD_SIZE and binds it to its own
+    GPU-local cores, and the line reports each rank's placement and host
+    phases (host_ranks)."""
     env = dict(os.environ, LDT_BENCH_BACKEND="gloo")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-                        "--no-cpu-baseline", "--dataset-batches", "2", "--dataset-epochs", "1"],
-                       cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
+                        os.path.join(REPO, "bench.py"), "--gpus", str(ranks), "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--dataset-batches", "2", "--dataset-epochs", "1", "--host-reps", "1"],
+                       cwd=REPO, capture_output=True, text=True, timeout=840, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["per_gpu_batch"]
-    assert abs(d["value_per_gpu"] - d["value"] / 2) <= 0.11
+    assert d["n_gpus"] == ranks and d["config"]["global_batch"] == ranks * d["config"]["per_gpu_batch"]
+    assert abs(d["value_per_gpu"] - d["value"] / ranks) <= 0.11
     for cw, per_rank in (("c3", 2), ("c4", None)):
         leg = d["config_legs"][cw]
-        assert leg["value_per_gpu"] * 2 == pytest.approx(leg["value"], abs=0.2)
+        assert leg["value_per_gpu"] * ranks == pytest.approx(leg["value"], abs=0.2)
         info = leg["dataset_leg"]
         assert info["images_all_ranks"] > 0 and info["epochs"] == 1
         if per_rank:
             # ShardedBatchSampler: every rank reads its `per_rank` batches of 128
-            assert info["images_all_ranks"] == 2 * per_rank * 128
+            assert info["images_all_ranks"] == ranks * per_rank * 128
+    hr = d["host_ranks"]
+    assert [h["rank"] for h in hr] == list(range(ranks))
+    for h in hr:
+        assert h["local_world"] == ranks and set(h["host_us_per_call"]) >= {"parse", "copy_join"}
+        assert h["copy_threads"] == len(h["copy_cpus"])
+    # ranks that share a NUMA node never share a copy core
+    used = [c for h in hr for c in h["copy_cpus"] if c >= 0]
+    assert len(used) == len(set(used)) or len(used) > 64, used

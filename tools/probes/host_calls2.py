@@ -1,7 +1,8 @@
 """Diagnostic (not a test): where the host time of the pipelined to_tensor_fn
 goes, per call: the ticket check (check_slot), the C decode call
 (decode_arrow) and the rest of the Python wrapper, plus the C++ host phases.
-usage: python host_calls2.py [c2] [depth] [reg|copy] [copy threads]"""
+usage: python host_calls2.py [c2] [depth] [reg|copy] [copy threads]
+env LDT_P_MODE / LDT_P_BIND / LDT_P_NT: LDT_OPT_COPY_MODE / _BIND / _NT."""
 import os
 import sys
 import time
@@ -49,6 +50,9 @@ fn = ldt_amd.make_to_tensor_fn(depth=depth, device=dev, register=len(sys.argv) >
 fn.pipeline.set_option(_lib.OPT_HOST_TIMING, 1)
 if len(sys.argv) > 4:
     fn.pipeline.set_option(_lib.OPT_COPY_THREADS, int(sys.argv[4]))
+for env, opt in (("LDT_P_MODE", _lib.OPT_COPY_MODE), ("LDT_P_BIND", _lib.OPT_COPY_BIND), ("LDT_P_NT", _lib.OPT_COPY_NT)):
+    if os.environ.get(env):
+        fn.pipeline.set_option(opt, int(os.environ[env]))
 for i in range(12):
     fn(bs[i % 2])
 torch.cuda.synchronize()
@@ -71,4 +75,5 @@ print(f"[{' '.join(sys.argv[1:])}] {N} calls: host loop {(t1 - t0) * 1e6 / N:.1f
 print(f"  per call: check_slot {acc['check'] * 1e6 / N:.1f}, decode_arrow {acc['decode_arrow'] * 1e6 / N:.1f}, "
       f"rest {(t1 - t0 - acc['check'] - acc['decode_arrow']) * 1e6 / N:.1f} us")
 print("  C++ phases us/call " + " ".join(f"{k}={v / max(n, 1):.1f}" for k, v in us.items()))
+print("  host_info", fn.pipeline.ctxs[0].host_info())
 print("  wall percentiles us", [round(float(np.percentile(walls, q)) * 1e6, 1) for q in (10, 50, 90, 99)])
