@@ -213,6 +213,9 @@ def main():
                     help="skip the configs[2]/configs[3] dataset legs (c3, c4) of a c2 run")
     ap.add_argument("--no-registered", action="store_true",
                     help="skip the host leg with the cell buffers page-locked in place (ldt_register_host)")
+    ap.add_argument("--only-resident", action="store_true",
+                    help="the resident leg alone (no host, dataset, config or standalone legs): the run a "
+                         "rocprofv3 --stats summary of the line's timed launches is taken from")
     ap.add_argument("--host-depth", type=int, default=2,
                     help="batches in flight of the host-input legs (make_to_tensor_fn(depth)): with the cells' "
                          "copy stream, depth + 2 streams fit the process's 4 hardware queues at depth 2")
@@ -352,9 +355,11 @@ def main():
             fn.release()
         return B * args.steps * world / t, {k_: round(v / max(calls, 1), 1) for k_, v in us.items()}, info
 
+    if args.only_resident:
+        args.dataset_batches = 0
     value_host = value_registered = host_us = host_info = None
     host_reps = []
-    if args.workload != "c5":
+    if args.workload != "c5" and not args.only_resident:
         # the copying leg (the plug-in contract: fresh host batches every call)
         # `host_reps` times back to back; value_host_input = the median
         for _ in range(max(1, args.host_reps)):
@@ -408,7 +413,7 @@ def main():
 
     # standalone launch durations (one batch in flight, after the timed region)
     standalone = None
-    if args.workload != "c5" and not args.no_stage_events:
+    if args.workload != "c5" and not args.no_stage_events and not args.only_resident:
         solo = ldt_amd.DecodePipeline(depth=1, device=dev, profile=True)
         solo.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
         for k in range(3):
@@ -619,7 +624,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     return tot_imgs / t, info
 
 
-PROFILE_ROUND = "r3"  # committed PMC summaries: this round's, else the newest earlier one
+PROFILE_ROUND = "r4"  # committed PMC summaries: this round's, else the newest earlier one
 
 
 def stream_copy_ceiling(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:

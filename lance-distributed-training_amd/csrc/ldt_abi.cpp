@@ -136,6 +136,7 @@ struct ldt_ctx {
   int64_t stage_cnt[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
   EvSet *cur_ev = nullptr;
   int64_t last_off_redo = -1; // debug counters of the last batch (plan blob offset)
+  uint8_t *last_plan_dev = nullptr; // that batch's plan blob on the device
   double host_us[kHpCount] = {};
   int64_t host_calls = 0;
 };
@@ -452,7 +453,9 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
     if (reg) {
       if ((rc = enqueue_cells(c, sl, cells_host, (size_t)total_bytes, s))) return rc;
     } else {
-      if ((rc = ensure_pin_slots(c, c->h_data, sl, (size_t)total_bytes + 16))) return rc;
+      // room for the plan blob after the cells (plan_with_cells below)
+      const size_t room = (size_t)total_bytes + 16 + std::max<size_t>((size_t)total_bytes / 8, (size_t)1 << 18);
+      if ((rc = ensure_pin_slots(c, c->h_data, sl, room))) return rc;
       CopyPool &pool = copier(c);
       pool.start(c->h_data[sl].p, cells_host, (size_t)total_bytes);
       cj.p = &pool;
@@ -853,8 +856,20 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   ph.max_blocks = max_blocks;
   ph.total_blocks = coef_blocks;
 
-  if ((rc = ensure_pin_slots(c, c->h_plan, sl, (size_t)plan_bytes))) return rc;
-  uint8_t *hp = static_cast<uint8_t *>(c->h_plan[sl].p);
+  // Host cells copied into the pinned slot: the plan blob follows them in the
+  // slot and reaches HBM in the same DMA (a separate small H2D copy would be
+  // enqueued behind the stream's wait for that DMA, and the runtime may
+  // perform small copies synchronously). Otherwise its own pinned buffer and
+  // copy on `s`.
+  const int64_t plan_off = align_up(total_bytes + 16, 256);
+  const bool plan_with_cells = cj.p != nullptr && (int64_t)c->h_data[sl].cap >= plan_off + plan_bytes;
+  uint8_t *hp;
+  if (plan_with_cells) {
+    hp = static_cast<uint8_t *>(c->h_data[sl].p) + plan_off;
+  } else {
+    if ((rc = ensure_pin_slots(c, c->h_plan, sl, (size_t)plan_bytes))) return rc;
+    hp = static_cast<uint8_t *>(c->h_plan[sl].p);
+  }
   memcpy(hp, &ph, sizeof(ph));
   memcpy(hp + ph.off_desc, D.data(), sizeof(ImgDesc) * (size_t)n);
   if (!S.empty()) memcpy(hp + ph.off_seg, S.data(), sizeof(Segment) * S.size());
@@ -872,7 +887,11 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if (!prog_img.empty()) memcpy(hp + off_pimg, prog_img.data(), 4 * prog_img.size());
 
   // ---- device workspace ----
-  if ((rc = ensure_dev(c, c->d_plan, (size_t)plan_bytes, s))) return rc;
+  if (plan_with_cells) {
+    if ((rc = ensure_dev(c, c->d_data[sl], (size_t)(plan_off + plan_bytes), s))) return rc;
+  } else if ((rc = ensure_dev(c, c->d_plan, (size_t)plan_bytes, s))) {
+    return rc;
+  }
   // slack: a decoder finishing its last block may read a few hundred bytes
   // past an image's region
   if ((rc = ensure_dev(c, c->d_dstuf, (size_t)dst_total + 1024, s))) return rc;
@@ -897,18 +916,20 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
         c->host_us[kHpCopyWake] += std::max(0.0, pool->last_wake_us());
         c->host_us[kHpCopySpan] += pool->last_span_us();
       }
-      if ((rc = enqueue_cells(c, sl, c->h_data[sl].p, (size_t)total_bytes, s))) return rc;
+      const size_t nb = (size_t)(plan_with_cells ? plan_off + plan_bytes : total_bytes);
+      if ((rc = enqueue_cells(c, sl, c->h_data[sl].p, nb, s))) return rc;
     }
     host_release(reg);
     dev_cells = static_cast<const uint8_t *>(c->d_data[sl].p);
   }
-  HIPCHK(c, hipMemcpyAsync(c->d_plan.p, hp, (size_t)plan_bytes, hipMemcpyHostToDevice, s));
+  if (!plan_with_cells) HIPCHK(c, hipMemcpyAsync(c->d_plan.p, hp, (size_t)plan_bytes, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipEventRecord(c->slot_ev[sl], s));
   c->slot_used[sl] = true;
   prof_mark(c, LDT_STAGE_H2D, s);
   ht.mark(kHpCopy);
 
-  uint8_t *dp = static_cast<uint8_t *>(c->d_plan.p);
+  uint8_t *dp = plan_with_cells ? static_cast<uint8_t *>(c->d_data[sl].p) + plan_off
+                                : static_cast<uint8_t *>(c->d_plan.p);
   DevPlan p;
   p.descs = reinterpret_cast<const ImgDesc *>(dp + ph.off_desc);
   p.segs = reinterpret_cast<Segment *>(dp + ph.off_seg);
@@ -946,6 +967,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.pscans = reinterpret_cast<const ProgScan *>(dp + off_pscan);
   p.ptabs = reinterpret_cast<const ProgTab *>(dp + off_ptab);
   c->last_off_redo = off_redo;
+  c->last_plan_dev = dp;
   DevWork w;
   w.data = dev_cells;
   w.dstuf = static_cast<uint8_t *>(c->d_dstuf.p);
@@ -1438,7 +1460,7 @@ int ldt_debug_counters(ldt_ctx *c, int32_t *out16, void *stream) {
   DeviceGuard g(c->device);
   if (c->last_off_redo < 0) return set_err(c, LDT_ERR_ARG, "no batch yet");
   HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-  HIPCHK(c, hipMemcpy(out16, static_cast<uint8_t *>(c->d_plan.p) + c->last_off_redo, 64,
+  HIPCHK(c, hipMemcpy(out16, c->last_plan_dev + c->last_off_redo, 64,
                       hipMemcpyDeviceToHost));
   return LDT_OK;
 }

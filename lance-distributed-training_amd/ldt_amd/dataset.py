@@ -223,6 +223,14 @@ class LanceDataset(IterableDataset):
                 raise RuntimeError("LanceDataset workers need multiprocessing_context='spawn' with this "
                                    "build's samplers (the batch plan runs device kernels in the main process)")
             if plan is None:
+                # a protocol sampler has no read plan to shard before reading:
+                # every worker runs it whole and keeps its own share, so the
+                # rows are read num_workers times (the decode is not repeated)
+                if info.id == 0 and info.num_workers > 1:
+                    import warnings
+
+                    warnings.warn(f"{type(sampler).__name__} has no read_plan: each of the {info.num_workers} "
+                                  "workers reads every batch and keeps 1/num_workers of them", RuntimeWarning)
                 batches = sampler(self.dataset, batch_size=self.batch_size, columns=self.columns,
                                   batch_readahead=self.batch_readahead)
                 for k, rb in enumerate(batches):

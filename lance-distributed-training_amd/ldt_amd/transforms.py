@@ -776,6 +776,12 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
     image_column = fixed.get("image_column", "image")
     owned: "OrderedDict[int, object]" = OrderedDict()  # registrations made here, LRU order
     reg_on = [bool(register)]
+    # churn guard: unregistering synchronises the device, so a loader that hands
+    # out fresh buffers every batch (instead of slices of mapped fragments)
+    # must not evict on every call; `evictions` holds the call numbers of the
+    # recent evictions
+    calls = [0]
+    evictions: list = []
 
     def maybe_register(batch, col):
         if not reg_on[0] or not isinstance(batch, pa.RecordBatch):
@@ -795,11 +801,22 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
             reg_on[0] = False  # copying path from here on
             return
         owned[addr] = arr
-        while len(owned) > max(1, int(register_cap)):
+        cap = max(1, int(register_cap))
+        while len(owned) > cap:
             _, old = owned.popitem(last=False)
             unregister_host(old)
+            evictions.append(calls[0])
+        # more evictions than the cap within 4 x cap calls: the buffers do not
+        # repeat, so registration cannot amortise; the copying path from here
+        # on (the ranges still registered are released at once)
+        while evictions and evictions[0] < calls[0] - 4 * cap:
+            evictions.pop(0)
+        if len(evictions) > cap:
+            reg_on[0] = False
+            release()
 
     def to_tensor_fn(batch, **kwargs):
+        calls[0] += 1
         maybe_register(batch, kwargs.get("image_column", image_column))
         pipe.check_slot(pipe.k % pipe.depth)
         img, lbl = pipe.decode(batch, normalize=kwargs.get("normalize", normalize),
@@ -814,6 +831,7 @@ def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int
             unregister_host(old)
 
     to_tensor_fn.check = pipe.check
+    to_tensor_fn.registering = lambda: reg_on[0]
     to_tensor_fn.pipeline = pipe
     to_tensor_fn.release = release
     to_tensor_fn.prefetch = max(0, min(int(prefetch), depth - 1))

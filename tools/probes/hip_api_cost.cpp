@@ -148,6 +148,27 @@ int main() {
     CK(hipDeviceSynchronize());
     printf("copy-stream handoff (wait, 17MB DMA, record, wait, 6 launches, record) (%s): %.1f us\n", tag, t / R);
   }
+  // a small H2D copy (the plan blob, 100 KB) enqueued on a stream that waits
+  // for an event of a copy stream still busy with a 17 MB DMA: does the
+  // enqueue block the host until the event fires?
+  for (size_t small : {(size_t)4 << 10, (size_t)100 << 10, (size_t)1 << 20}) {
+    double t = 0, tw = 0;
+    for (int r = 0; r < 10; ++r) {
+      CK(hipMemcpyAsync(d2, h, N, hipMemcpyHostToDevice, s[4]));
+      CK(hipEventRecord(ev[r % 64], s[4]));
+      CK(hipStreamWaitEvent(s[1], ev[r % 64], 0));
+      double a = now_us();
+      CK(hipMemcpyAsync(d, h, small, hipMemcpyHostToDevice, s[1]));
+      double b = now_us();
+      k_nop<<<1, 64, 0, s[1]>>>(sink);
+      double c = now_us();
+      t += b - a;
+      tw += c - b;
+      CK(hipDeviceSynchronize());
+    }
+    printf("H2D %zu KB on a stream waiting for a busy copy stream: enqueue %.1f us, next launch %.1f us\n",
+           small >> 10, t / 10, tw / 10);
+  }
   // how long a 17MB DMA takes while 3 streams run kernels
   {
     hipEvent_t a, z;

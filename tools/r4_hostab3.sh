@@ -6,6 +6,9 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-r4ab3}
 mkdir -p $O
 cd $R
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullbatch.py tests/test_gpu_loaders.py -x -q --timeout 120 --timeout-method thread -k "copy or pipelined or registered or status or golden or fullbatch or prefetch or loader or register or huffman_decoder" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 120 ./tools/probes/hip_api_cost > $O/hip_api_cost.txt 2>&1 && grep "waiting for a busy" $O/hip_api_cost.txt
 for rep in 1 2 3; do
   for hd in 2 3; do
     timeout -k 10 300 python3 bench.py --no-cpu-baseline --dataset-batches 0 --steps 60 --warmup 10 --host-depth $hd > $O/b_d${hd}_$rep.json 2> $O/b_d${hd}_$rep.err || { tail -5 $O/b_d${hd}_$rep.err; exit 1; }
