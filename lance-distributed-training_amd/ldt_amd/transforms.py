@@ -745,12 +745,14 @@ class DecodePipeline:
             raise ImageDecodeError(bad)
 
 
-def make_to_tensor_fn(depth: int = 3, device=None, normalize=None, prefetch: int = 0,
+def make_to_tensor_fn(depth: int = 2, device=None, normalize=None, prefetch: int = 0,
                       register: bool = False, register_cap: int = 8, **fixed):
     """A pipelined ``to_tensor_fn`` for ``LanceDataset(..., to_tensor_fn=...)``
     (lance_iterable.py:53-59): each call enqueues its RecordBatch on one of
     `depth` contexts/streams and returns at once, so batch k+1's host copy and
-    kernels overlap batch k's. The tensors are ready on torch's current stream
+    kernels overlap batch k's. Depth 2 (the default) leaves the cells' copy
+    stream its own hardware queue (DecodePipeline): measured faster on host
+    batches than depth 3 with the DMA on the slot streams. The tensors are ready on torch's current stream
     (it waits for the slot's stream). Per-image errors are reported
     asynchronously: by ``fn.check()``, and at the latest when the slot is
     reused a second time (2 * `depth` calls later, when that batch finished
