@@ -590,7 +590,10 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     # the fragments are memory-mapped Arrow IPC files whose image buffers live
     # as long as the dataset: page-locked once per fragment (register=True),
     # every batch sliced from them is DMAed without a host copy
-    fn = ldt_amd.make_to_tensor_fn(depth=args.host_depth, device=dev, register=not args.dataset_copy)
+    # 3 in flight as the resident leg: the configs' batches of 128 need the
+    # concurrency more than the copy stream (DMA on the slot streams here,
+    # DecodePipeline's choice at depth 3)
+    fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev, register=not args.dataset_copy)
     fn.pipeline.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
     ds = ldt_amd.LanceDataset(path, batch_size=B, sampler=sampler, to_tensor_fn=fn)
 
@@ -625,7 +628,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
             "images_all_ranks": tot_imgs, "elapsed_ms_max": round(t * 1e3, 3),
             "timing": "full epochs per rank (plan + every batch, padding included) between barriers, "
                       "max over ranks",
-            "harness": (f"LanceDataset(path, batch_size, sampler, to_tensor_fn=make_to_tensor_fn(depth={args.host_depth}, "
+            "harness": (f"LanceDataset(path, batch_size, sampler, to_tensor_fn=make_to_tensor_fn(depth={args.depth}, "
                         f"register={not args.dataset_copy}))")}
     return tot_imgs / t, info
 
