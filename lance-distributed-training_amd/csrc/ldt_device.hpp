@@ -206,14 +206,14 @@ __host__ __device__ __forceinline__ uint32_t ds_ff4(uint32_t w) { // bit i: byte
   const uint32_t h = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
   return (((h >> 7) * 0x204081u) >> 21) & 0xFu;
 }
-__host__ __device__ __forceinline__ uint32_t ds_byte(const uint32_t wv[6], int k) { // k < 24
+// Byte k < 24 of the six words, by bit tests on the word index (a select
+// chain over an array's elements is folded into a dynamically indexed load,
+// which puts the words in scratch memory)
+__host__ __device__ __forceinline__ uint32_t ds_byte(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                                     uint32_t w4, uint32_t w5, int k) {
   const int q = k >> 2;
-  uint32_t w = wv[0];
-  w = q == 1 ? wv[1] : w;
-  w = q == 2 ? wv[2] : w;
-  w = q == 3 ? wv[3] : w;
-  w = q == 4 ? wv[4] : w;
-  w = q == 5 ? wv[5] : w;
+  const uint32_t a = (q & 1) ? w1 : w0, b = (q & 1) ? w3 : w2, c = (q & 1) ? w5 : w4;
+  const uint32_t w = (q & 4) ? c : ((q & 2) ? b : a);
   return (w >> (8 * (k & 3))) & 255u;
 }
 __host__ __device__ __forceinline__ void ds_classify16_ff(const uint32_t wv[6], int64_t p0, int64_t L,
@@ -225,16 +225,16 @@ __host__ __device__ __forceinline__ void ds_classify16_ff(const uint32_t wv[6], 
   keep = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
   rst = 0;
   local_end = 16;
-  uint32_t ff = 0;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) ff |= ds_ff4(wv[i]) << (4 * i);
+  const uint32_t w0 = wv[0], w1 = wv[1], w2 = wv[2], w3 = wv[3], w4 = wv[4], w5 = wv[5];
+  const uint32_t ff = ds_ff4(w0) | (ds_ff4(w1) << 4) | (ds_ff4(w2) << 8) | (ds_ff4(w3) << 12) |
+                      (ds_ff4(w4) << 16) | (ds_ff4(w5) << 20);
   // 0xFF bytes from the one before the lane's first (bit 0) to its last (16)
   uint32_t m = (ff >> 3) & 0x1FFFFu;
   while (m) {
     const int b = __builtin_ctz(m);
     m &= m - 1u;
     const int j = b - 1; // the 0xFF's byte (-1: the previous lane's last)
-    const uint32_t nx_raw = ds_byte(wv, b + 4);
+    const uint32_t nx_raw = ds_byte(w0, w1, w2, w3, w4, w5, b + 4);
     if (j >= 0) {
       const int64_t p = p0 + j;
       const bool in = p >= 0 && p < L;

@@ -194,13 +194,30 @@ __device__ __forceinline__ int image_slots(const ImgDesc &d, uint32_t &slotmap, 
 constexpr int kTabPieces = (kLcBytes + kL2Bytes) / 16; // HuffTab: lc then l2
 typedef uint32_t v4u __attribute__((ext_vector_type(4))); // 16-byte piece (LDS-storable)
 static_assert(sizeof(HuffTab) % 16 == 0, "16-byte table pieces");
-__device__ __forceinline__ const v4u *tab_piece_src(const HuffTab *__restrict__ htabs,
-                                                      const int *slot_tab, int i, int &dst, int ns) {
-  const int q = i / kTabPieces, o = i - q * kTabPieces;
-  int tix = slot_tab[0];
+// The plan-table index of each of an image's (at most 6) slots, 16 bits
+// each, packed into integers: picking one by a variable slot is shifts, where
+// an int[6] picked by a select chain is folded into a dynamically indexed
+// load that puts the array in scratch memory.
+struct SlotTabs {
+  uint64_t lo; // slots 0-3
+  uint32_t hi; // slots 4-5
+  __device__ __forceinline__ int get(int q) const {
+    return (int)(q < 4 ? (lo >> (16 * q)) & 0xFFFFu : (hi >> (16 * (q - 4))) & 0xFFFFu);
+  }
+};
+__device__ __forceinline__ SlotTabs pack_slots(const int *slot_tab) {
+  SlotTabs t;
+  t.lo = 0;
+  t.hi = 0;
 #pragma unroll
-  for (int x = 1; x < 6; ++x)
-    if (q == x) tix = slot_tab[x];
+  for (int x = 0; x < 4; ++x) t.lo |= (uint64_t)(slot_tab[x] & 0xFFFF) << (16 * x);
+  t.hi = (uint32_t)(slot_tab[4] & 0xFFFF) | ((uint32_t)(slot_tab[5] & 0xFFFF) << 16);
+  return t;
+}
+__device__ __forceinline__ const v4u *tab_piece_src(const HuffTab *__restrict__ htabs,
+                                                      const SlotTabs &st, int i, int &dst, int ns) {
+  const int q = i / kTabPieces, o = i - q * kTabPieces;
+  const int tix = st.get(q);
   dst = o < kLcBytes / 16 ? (q << 13) + 16 * o : (ns << 13) + q * kL2Bytes + 16 * o - kLcBytes;
   return reinterpret_cast<const v4u *>(htabs + tix) + o;
 }
@@ -209,21 +226,19 @@ __device__ __forceinline__ const v4u *tab_piece_src(const HuffTab *__restrict__ 
 // (k_huff_image stages them itself, together with the stream window).
 __device__ __forceinline__ Dec load_dec(const ImgDesc &d, const HuffTab *__restrict__ htabs,
                                         LDS_AS uint8_t *tabs, int tid, int nthreads,
-                                        bool copy = true, int *slot_tab_out = nullptr) {
+                                        bool copy = true, SlotTabs *slot_tab_out = nullptr) {
   int slot_tab[6];
   uint32_t slotmap;
   const int ns = image_slots(d, slotmap, slot_tab);
+  const SlotTabs stp = pack_slots(slot_tab);
   if (copy) {
     for (int i = tid; i < ns * kTabPieces; i += nthreads) {
       int dst;
-      const v4u v = *tab_piece_src(htabs, slot_tab, i, dst, ns);
+      const v4u v = *tab_piece_src(htabs, stp, i, dst, ns);
       *(LDS_AS v4u *)(tabs + dst) = v;
     }
   }
-  if (slot_tab_out) {
-#pragma unroll
-    for (int x = 0; x < 6; ++x) slot_tab_out[x] = slot_tab[x];
-  }
+  if (slot_tab_out) *slot_tab_out = stp;
   Dec dec;
   dec.tabs = tabs;
   dec.dcseq = dec.acseq = 0;
@@ -1091,6 +1106,10 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
 // uniform) for a corrupt image, with status 3 as k_destuff_layout sets it.
 // ---------------------------------------------------------------------------
 constexpr int kFuseTile = 16 * kHuffThreads;
+#ifndef LDT_FUSE_PRE
+#define LDT_FUSE_PRE 2
+#endif
+constexpr int kFusePre = LDT_FUSE_PRE; // tiles whose loads are in flight together
 template <class Pre>
 __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ data, const ImgDesc &d,
                                                     LDS_AS uint8_t *win, ImgLds &sh, int tid,
@@ -1119,12 +1138,11 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
     }
   };
   auto put = [&](int o, uint32_t v) { win[o ^ 3] = (uint8_t)v; };
-  uint32_t wv[6], nx[6];
-  load(0, wv);
-  after_first_load(); // the caller's table stores: their loads were issued first
   int K = 0, R = 0; // kept bytes and RSTn markers of the earlier tiles
-  for (int64_t cb = 0; cb < span; cb += kFuseTile) {
-    load(cb + kFuseTile, nx); // the next tile (clamped past the end)
+  // One tile: classify the lane's 16 bytes, find the tile's first end-of-scan
+  // marker, compact the kept bytes into the window. Returns true at the end
+  // of the scan (workgroup-uniform).
+  auto tile = [&](int64_t cb, const uint32_t wv[6]) __attribute__((always_inline)) -> bool {
     const int64_t p0 = cb + 16 * tid - lead;
     uint32_t keep, rst;
     int le;
@@ -1178,9 +1196,21 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
     }
     K += tot & 0xFFFF;
     R += tot >> 16;
-    if (ended) break;
+    return ended;
+  };
+  // The tiles' loads go out kFusePre tiles at a time (c2's ~67 KB streams:
+  // all five in the first group), so the global-load latency is paid once per
+  // group instead of once per tile behind a one-tile prefetch; the compaction
+  // stays tile by tile, in order.
+  bool done = false;
+  for (int64_t g0 = 0; g0 < span && !done; g0 += kFusePre * kFuseTile) {
+    uint32_t wv[kFusePre][6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) wv[i] = nx[i];
+    for (int t = 0; t < kFusePre; ++t) load(g0 + t * kFuseTile, wv[t]);
+    if (g0 == 0) after_first_load(); // the caller's table stores: their loads were issued first
+#pragma unroll
+    for (int t = 0; t < kFusePre; ++t)
+      if (!done && g0 + t * kFuseTile < span) done = tile(g0 + t * kFuseTile, wv[t]);
   }
   if (R != last) { // restart markers do not match the header
     if (tid == 0) status[img] = 3;
@@ -1235,8 +1265,8 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   const uint64_t t_start = wall_clock64();
   // dynamic LDS: [window win_bytes][tables]
   LDS_AS uint8_t *tabs = (LDS_AS uint8_t *)(dyn_lds + win_bytes / 4);
-  int slot_tab[6];
-  const Dec dec = load_dec(d, htabs, tabs, tid, kHuffThreads, false, slot_tab);
+  SlotTabs slot_tab;
+  const Dec dec = load_dec(d, htabs, tabs, tid, kHuffThreads, false, &slot_tab);
   const bool fused = d.ds_count == 0;
   for (int s = tid; s < d.nseg && !fused; s += kHuffThreads) {
     const Segment &sg = segs[d.seg_base + s];
@@ -1289,7 +1319,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     v4u tv[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) // slot q's pieces on lanes 0..kTabPieces-1 (q is uniform)
-      tv[q] = reinterpret_cast<const v4u *>(htabs + slot_tab[q < ns ? q : 0])[otab];
+      tv[q] = reinterpret_cast<const v4u *>(htabs + slot_tab.get(q < ns ? q : 0))[otab];
     const v4u *gsrc = reinterpret_cast<const v4u *>(base);
     LDS_AS v4u *wl = (LDS_AS v4u *)dyn_lds;
     const int nwin = in_lds ? (int)(need / 16) : 0;
