@@ -1106,10 +1106,6 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
 // uniform) for a corrupt image, with status 3 as k_destuff_layout sets it.
 // ---------------------------------------------------------------------------
 constexpr int kFuseTile = 16 * kHuffThreads;
-#ifndef LDT_FUSE_PRE
-#define LDT_FUSE_PRE 2
-#endif
-constexpr int kFusePre = LDT_FUSE_PRE; // tiles whose loads are in flight together
 template <class Pre>
 __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ data, const ImgDesc &d,
                                                     LDS_AS uint8_t *win, ImgLds &sh, int tid,
@@ -1198,19 +1194,18 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
     R += tot >> 16;
     return ended;
   };
-  // The tiles' loads go out kFusePre tiles at a time (c2's ~67 KB streams:
-  // all five in the first group), so the global-load latency is paid once per
-  // group instead of once per tile behind a one-tile prefetch; the compaction
-  // stays tile by tile, in order.
-  bool done = false;
-  for (int64_t g0 = 0; g0 < span && !done; g0 += kFusePre * kFuseTile) {
-    uint32_t wv[kFusePre][6];
+  // one tile's loads in flight while the one before it is compacted (issuing
+  // two or three tiles at a time saved 3 of the ~25 us of a c2 image's setup
+  // but raised the kernel to 110-128 VGPRs, and the pipeline lost more than
+  // that: profiles/r4/huffvar_r4hv.txt)
+  uint32_t wv[6], nx[6];
+  load(0, wv);
+  after_first_load(); // the caller's table stores: their loads were issued first
+  for (int64_t cb = 0; cb < span; cb += kFuseTile) {
+    load(cb + kFuseTile, nx); // the next tile (clamped past the end)
+    if (tile(cb, wv)) break;
 #pragma unroll
-    for (int t = 0; t < kFusePre; ++t) load(g0 + t * kFuseTile, wv[t]);
-    if (g0 == 0) after_first_load(); // the caller's table stores: their loads were issued first
-#pragma unroll
-    for (int t = 0; t < kFusePre; ++t)
-      if (!done && g0 + t * kFuseTile < span) done = tile(g0 + t * kFuseTile, wv[t]);
+    for (int i = 0; i < 6; ++i) wv[i] = nx[i];
   }
   if (R != last) { // restart markers do not match the header
     if (tid == 0) status[img] = 3;

@@ -30,6 +30,8 @@ if [ "$2" = "A" ]; then
   python3 $R/tools/traffic_all.py $O/traffic > $O/traffic_c2_perkernel.txt && cat $O/traffic_c2_perkernel.txt
   python3 $R/tools/traffic_summary.py $O/traffic c2 > $O/traffic_c2.json
 else
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullbatch.py -x -q --timeout 120 --timeout-method thread -k "fused or corrupt or golden or config_batches or fullbatch or huffman or restart or marker or progressive" > $O/pytest_b.log 2>&1 || { tail -30 $O/pytest_b.log; exit 1; }
+  tail -1 $O/pytest_b.log
   PROBE=../tools/probes/pmc_c2.py bash $R/tools/pmc.sh ${T}_dec c2 1 2 3 > /dev/null || exit 1
   python3 $R/tools/decode_eff.py $R/gpurun_out/pmc_${T}_dec c2 > $O/pmc_c2_decode.json
   for w in c1 c4 c5 c2p; do
