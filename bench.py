@@ -347,7 +347,9 @@ def main():
             fn(bs[k[0] % len(bs)])
             k[0] += 1
 
-        for _ in range(warm if fresh else 2 * args.host_depth):
+        # a fresh function's first steps allocate its pinned slots and start
+        # its copy pool: at least 50 untimed steps before the first timed leg
+        for _ in range(max(warm, 50) if fresh else 2 * args.host_depth):
             hstep()
         barrier()
         fn.pipeline.host_times(reset=True)
