@@ -71,7 +71,9 @@ extern "C" {
                                  sources wider than 1120 px; 2: the streaming
                                  kernel for all (cross-check); 3: 4:2:0 sources
                                  <= 512 px wide two waves per band
-                                 (k_resize420, cross-check; slower)          */
+                                 (k_resize420, cross-check; slower); 4: the
+                                 same sources one staged row per step, 4 waves
+                                 per SIMD (k_resize4r, cross-check; no faster) */
 #define LDT_OPT_SYNC_WARM 7   /* parallel decoder phase 1 starts this % of S
                                  before each range (0..200, default 0)         */
 #define LDT_OPT_COPY_THREADS 8 /* threads of the context's host copy pool that

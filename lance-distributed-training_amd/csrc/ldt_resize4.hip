@@ -166,19 +166,24 @@ constexpr int kResizeWaves = 2;
 // the waitcnt pass never sees another path's loads pending at the loop's
 // merge points (that forced a vmcnt(0) ahead of the horizontal taps and
 // serialised the prefetch).
+// SRC 4: the 4:2:0 fast path staging ONE source row per step (k_resize4r):
+// half the staging LDS and registers of SRC 0, so that a 2-wave workgroup
+// fits 20 KB and 4 waves per SIMD (128 VGPRs); the last horizontal job then
+// covers columns 192-223 with half the wave.
 template <int SRC, int KS>
-__global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ descs,
-                                                 const uint8_t *__restrict__ planes, RawSrc raw,
-                                                 const float *__restrict__ lut,
-                                                 const int64_t *__restrict__ labels,
-                                                 float *__restrict__ out,
-                                                 int64_t *__restrict__ out_labels,
-                                                 const int32_t *__restrict__ status, Geom4 g) {
+__device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
+                                             const uint8_t *__restrict__ planes, RawSrc raw,
+                                             const float *__restrict__ lut,
+                                             const int64_t *__restrict__ labels,
+                                             float *__restrict__ out,
+                                             int64_t *__restrict__ out_labels,
+                                             const int32_t *__restrict__ status, const Geom4 &g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // Skewed staging for raw rows (c5: 4-5-way tap conflicts otherwise, and the
   // kernel is LDS-bound). JPEG rows stay plain: the skew's extra registers
   // cost a wave per SIMD there, which is worth more than its 2-way conflicts.
-  constexpr bool kJpeg = SRC == 0 || SRC == 2;
+  constexpr bool kJpeg = SRC == 0 || SRC == 2 || SRC == 4;
+  constexpr bool kRow = SRC == 4; // one staged row per step
   constexpr bool kSkew = !kJpeg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
@@ -199,7 +204,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
       for (int i = lane; i < per; i += 64) o[c * (kOut * kOut / 4) + i] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
-  if (kJpeg && resize_fast420(descs[img]) != (SRC == 0)) return;
+  if (kJpeg && resize_fast420(descs[img]) != (SRC == 0 || SRC == 4)) return;
   int W, H;
   if constexpr (kJpeg) {
     W = descs[img].width;
@@ -214,8 +219,8 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   if (band == 0 && lane == 0 && labels != nullptr) out_labels[img] = labels[img];
 
   uint8_t *wbase = smem + 3072 + wave * g.wave_bytes;
-  uint32_t *stg = reinterpret_cast<uint32_t *>(wbase);               // 2 * spad dwords
-  uint8_t *ring = wbase + 8 * g.spad;                                // 3 * ring * 224
+  uint32_t *stg = reinterpret_cast<uint32_t *>(wbase);               // 2 (kRow: 1) * spad dwords
+  uint8_t *ring = wbase + (kRow ? 4 : 8) * g.spad;                   // 3 * ring * 224
   int32_t *kv = reinterpret_cast<int32_t *>(ring + 3 * g.ring * kOut); // kKvRows * ks_v
   int32_t *vb = kv + kKvRows * g.ks_v;                               // kKvRows * 2
   const int ks_v = g.ks_v, RING = g.ring;
@@ -250,7 +255,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
     ya = ymin_a;
     yb = ymin_b + cnt_b;
   }
-  const int ya0 = kJpeg ? (ya & ~1) : ya;
+  const int ya0 = kJpeg && !kRow ? (ya & ~1) : ya;
 
   // vertical-pass items: 168 dwords (3 channels x 56 groups of 4 columns)
   int vc[3], vo[3];
@@ -262,7 +267,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   }
 
   // JPEG fast path: 4:2:0 with both chroma planes fancy-upsampled, W <= 512
-  constexpr bool fast420 = SRC == 0;
+  constexpr bool fast420 = SRC == 0 || SRC == 4;
   int rc = 5, cdh = 1;
   // plane geometry copied to registers once: the wave fences in process()
   // would otherwise make every fetch reload it (a dependent global round trip
@@ -294,7 +299,21 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   } pa;
   auto fetch = [&](Pre &pf, int y) {
     Jpair &jp = pf.jp;
-    if constexpr (kJpeg) {
+    if constexpr (kRow) {
+      // row y: 8 luma pixels, chroma rows cy and its fancy-upsampling
+      // neighbour (cy - 1 for an even row, cy + 1 for an odd one), 4 samples
+      const int x0 = lane * 8;
+      jp.y0 = x0 < W ? *reinterpret_cast<const uint2 *>(planes + po0 + (int64_t)y * ps0 + x0) : make_uint2(0, 0);
+      const int cy = y >> 1;
+      const int cn = (y & 1) ? min(cy + 1, cdh - 1) : max(cy - 1, 0);
+      const int cx0 = lane * 4;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const uint8_t *pc = planes + (c ? po2 : po1) + cx0;
+        jp.c[c][0] = cx0 < ps1 ? *reinterpret_cast<const uint32_t *>(pc + (int64_t)cy * ps1) : 0u;
+        jp.c[c][1] = cx0 < ps1 ? *reinterpret_cast<const uint32_t *>(pc + (int64_t)cn * ps1) : 0u;
+      }
+    } else if constexpr (kJpeg) {
       if constexpr (fast420) {
         const int x0 = lane * 8;
         const uint8_t *py = planes + po0 + (int64_t)y * ps0 + x0;
@@ -326,7 +345,38 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   auto stage = [&](const Pre &pf, int y) {
     const Jpair &jp = pf.jp;
     uint32_t *s0 = stg, *s1 = stg + g.spad;
-    if constexpr (kJpeg) {
+    if constexpr (kRow) {
+      // jdsample.c h2v2_fancy_upsample of row y (3 x the nearer chroma row +
+      // the farther one, then horizontally), jdcolor.c ycc_rgb_convert
+      const int x0 = lane * 8;
+      int up[2][8];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        int A[6], N[6], V[6];
+        bytes6(jp.c[c][0], lane, rc, A);
+        bytes6(jp.c[c][1], lane, rc, N);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) V[i] = A[i] * 3 + N[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int ci = (j >> 1) + 1;
+          const int nv = (j & 1) ? V[ci + 1] : V[ci - 1];
+          up[c][j] = (V[ci] * 3 + nv + 8 - (j & 1)) >> 4;
+        }
+      }
+      uint32_t px[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t yv = j < 4 ? jp.y0.x : jp.y0.y;
+        px[j] = ycc_px((int)((yv >> (8 * (j & 3))) & 255), up[0][j], up[1][j]);
+      }
+      if (x0 < W) {
+        uint4 *d0 = reinterpret_cast<uint4 *>(s0 + x0);
+        d0[0] = make_uint4(px[0], px[1], px[2], px[3]);
+        d0[1] = make_uint4(px[4], px[5], px[6], px[7]);
+      }
+      (void)s1;
+    } else if constexpr (kJpeg) {
       const ImgDesc &d = *dp;
       if constexpr (fast420) {
         const int x0 = lane * 8;
@@ -422,9 +472,11 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   auto horizontal = [&](int y) {
     const int slot1 = slot + 1 == RING ? 0 : slot + 1;
 #pragma unroll
-    for (int job = 0; job < 7; ++job) {
-      const int q = job < 6 ? job >> 1 : 3;
-      const int r = job < 6 ? (job & 1) : (lane >> 5);
+    for (int job = 0; job < (kRow ? 4 : 7); ++job) {
+      // kRow: jobs q = 0..3 of the one row (q = 3: both half-waves compute
+      // columns 192-223 and store the same bytes)
+      const int q = kRow ? job : (job < 6 ? job >> 1 : 3);
+      const int r = kRow ? 0 : (job < 6 ? (job & 1) : (lane >> 5));
       const int ox = q < 3 ? lane + 64 * q : 192 + (lane & 31);
       const uint32_t *rowp = stg + (r ? g.spad : 0);
       int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
@@ -445,7 +497,7 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
       rw[RING * kOut] = (uint8_t)min((uint32_t)a1 >> kPrecisionBits, 255u);
       rw[2 * RING * kOut] = (uint8_t)min((uint32_t)a2 >> kPrecisionBits, 255u);
     }
-    slot = slot1 + 1 == RING ? 0 : slot1 + 1;
+    slot = kRow ? slot1 : (slot1 + 1 == RING ? 0 : slot1 + 1);
   };
   // finish every output row whose vertical window lies in ring rows [ya0, done)
   auto vertical = [&](int done) {
@@ -506,16 +558,40 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   // of being waited for (vmcnt counts loads and stores together) by the next
   // staging's wait for its prefetched rows. The ring size is unchanged: the
   // rows still pending need at most ks_v - 1 earlier rows plus this pair.
+  constexpr int kStep = kRow ? 1 : 2;
   fetch(pa, ya0);
-  for (int y = ya0; y < yb; y += 2) {
+  for (int y = ya0; y < yb; y += kStep) {
     stage(pa, y);
-    if (y + 2 < yb) fetch(pa, y + 2);
+    if (y + kStep < yb) fetch(pa, y + kStep);
     wave_lds_fence();
     vertical(y);
     horizontal(y);
     wave_lds_fence();
   }
   vertical(yb + 1);
+}
+
+template <int SRC, int KS>
+__global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ descs,
+                                                 const uint8_t *__restrict__ planes, RawSrc raw,
+                                                 const float *__restrict__ lut,
+                                                 const int64_t *__restrict__ labels,
+                                                 float *__restrict__ out,
+                                                 int64_t *__restrict__ out_labels,
+                                                 const int32_t *__restrict__ status, Geom4 g) {
+  resize4_body<SRC, KS>(descs, planes, raw, lut, labels, out, out_labels, status, g);
+}
+
+// the single-row 4:2:0 variant, held to 128 VGPRs (4 waves per SIMD)
+template <int KS>
+__global__ void __launch_bounds__(128, 4) k_resize4r(const ImgDesc *__restrict__ descs,
+                                                     const uint8_t *__restrict__ planes, RawSrc raw,
+                                                     const float *__restrict__ lut,
+                                                     const int64_t *__restrict__ labels,
+                                                     float *__restrict__ out,
+                                                     int64_t *__restrict__ out_labels,
+                                                     const int32_t *__restrict__ status, Geom4 g) {
+  resize4_body<4, KS>(descs, planes, raw, lut, labels, out, out_labels, status, g);
 }
 
 // ---------------------------------------------------------------------------
@@ -764,17 +840,18 @@ __global__ void __launch_bounds__(128, 4) k_resize420(const ImgDesc *__restrict_
 // ---------------------------------------------------------------------------
 // Launch geometry.
 // ---------------------------------------------------------------------------
-static int wave_bytes4(const Geom4 &g) {
-  const int b = 8 * g.spad + 3 * g.ring * kOut + 4 * (kKvRows * g.ks_v + 2 * kKvRows);
+static int wave_bytes4(const Geom4 &g, int rows) {
+  const int b = 4 * rows * g.spad + 3 * g.ring * kOut + 4 * (kKvRows * g.ks_v + 2 * kKvRows);
   return (b + 15) & ~15;
 }
 
-static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g) {
+// rows: staged source rows per step (2; 1 for the single-row 4:2:0 kernel)
+static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g, int rows = 2) {
   g.ks_v = resample_ksize_host(max_h, kOut);
   g.ring = g.ks_v + 1; // an output row is finished within 2 rows of its window end
   const int px = ((max_w + 15) / 16) * 16 + ks_h + 16;
   g.spad = (px + ((px >> 5) << 2) + 4 + 3) & ~3; // skewed pixels (skw)
-  g.wave_bytes = wave_bytes4(g);
+  g.wave_bytes = wave_bytes4(g, rows);
   int nb = (waves_target + n - 1) / n;
   if (nb < 1) nb = 1;
   if (nb > 28) nb = 28;
@@ -812,9 +889,22 @@ static bool dispatch4(int ks_h, const ImgDesc *descs, const uint8_t *planes, Raw
   }
 }
 
+template <int KS>
+static hipError_t launch4r(const ImgDesc *descs, const uint8_t *planes, const float *lut, const int64_t *labels,
+                           float *out, int64_t *out_labels, const int32_t *status, const Geom4 &g, hipStream_t s) {
+  static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resize4r<KS>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  const int groups = (g.ntask + kResizeWaves - 1) / kResizeWaves;
+  hipLaunchKernelGGL((k_resize4r<KS>), dim3(groups), dim3(64 * kResizeWaves), 3072 + kResizeWaves * g.wave_bytes,
+                     s, descs, planes, RawSrc{nullptr, 0, 0, 0}, lut, labels, out, out_labels, status, g);
+  return hipGetLastError();
+}
+
 // Waves to aim for: the CU count times the resident waves per CU the LDS
-// allows (at most 12).
-static int waves_target4(const Geom4 &g, int pct) {
+// allows (at most 12; 16 for the single-row kernel, whose workgroups fit 8
+// per CU).
+static int waves_target4(const Geom4 &g, int pct, int max_wg = 6) {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
@@ -823,7 +913,7 @@ static int waves_target4(const Geom4 &g, int pct) {
     else cus = prop.multiProcessorCount;
   }
   int wg = (160 * 1024) / (3072 + kResizeWaves * g.wave_bytes);
-  if (wg > 6) wg = 6;
+  if (wg > max_wg) wg = max_wg;
   if (wg < 1) wg = 1;
   // LDT_OPT_RESIZE_WAVES_PCT: more, shorter bands fill the
   // pipeline's CU gaps better but cost the kernel's own efficiency
@@ -884,10 +974,27 @@ bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t
   // other's images); a batch of one kind launches one kernel. The first
   // launch also writes the failed images (k_fill_failed's job otherwise).
   g.fill = 1;
+  if (p.n_fast420 > 0 && p.resize420 == 2) {
+    // single-row 4:2:0 kernel (LDT_OPT_RESIZE_IMPL 4), W <= 512
+    Geom4 gr;
+    const int ks_f = resample_ksize_host(std::min(p.max_w, 512), kOut);
+    if (ks_f <= 7 && make_geom4(p.n, std::min(p.max_w, 512), p.max_h, ks_f, 1, gr, 1) &&
+        make_geom4(p.n, std::min(p.max_w, 512), p.max_h, ks_f, waves_target4(gr, p.resize_waves_pct, 8), gr, 1)) {
+      gr.fill = 1;
+      switch (ks_f) {
+      case 3: *err = launch4r<3>(p.descs, w.planes, p.lut, p.labels, out, out_labels, w.status, gr, s); break;
+      case 5: *err = launch4r<5>(p.descs, w.planes, p.lut, p.labels, out, out_labels, w.status, gr, s); break;
+      default: *err = launch4r<7>(p.descs, w.planes, p.lut, p.labels, out, out_labels, w.status, gr, s); break;
+      }
+      if (*err != hipSuccess || p.n_fast420 == p.n) return true;
+      g.fill = 0;
+      return dispatch4<2>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s, err);
+    }
+  }
   if (p.n_fast420 > 0) {
     GeomW2 g2;
     const int ks_f = resample_ksize_host(std::min(p.max_w, 512), kOut);
-    if (p.resize420 && make_geom_w2(p.n, std::min(p.max_w, 512), p.max_h, ks_f, p.resize_waves_pct, g2) &&
+    if (p.resize420 == 1 && make_geom_w2(p.n, std::min(p.max_w, 512), p.max_h, ks_f, p.resize_waves_pct, g2) &&
         ks_f <= 7) {
       // 4:2:0 images (width <= 512): two waves per band
       switch (ks_f) {
