@@ -201,8 +201,9 @@ def main():
                          "the per-GPU share of an 8-GPU node; 'all' = len(os.sched_getaffinity(0)))")
     ap.add_argument("--no-stage-events", action="store_true",
                     help="time without the per-stage HIP events (no roofline)")
-    ap.add_argument("--depth", type=int, default=3,
-                    help="batches in flight (ldt_amd.DecodePipeline: one context + HIP stream each)")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="batches in flight (ldt_amd.DecodePipeline: one context + HIP stream each); default 3, "
+                         "4 for progressive workloads (a c2p batch takes ~15 ms on the device)")
     ap.add_argument("--dataset-batches", type=int, default=12,
                     help="batches per rank of one epoch of the dataset leg (0: skip the leg)")
     ap.add_argument("--dataset-epochs", type=int, default=2,
@@ -216,15 +217,21 @@ def main():
     ap.add_argument("--only-resident", action="store_true",
                     help="the resident leg alone (no host, dataset, config or standalone legs): the run a "
                          "rocprofv3 --stats summary of the line's timed launches is taken from")
-    ap.add_argument("--host-depth", type=int, default=2,
-                    help="batches in flight of the host-input legs (make_to_tensor_fn(depth)): with the cells' "
-                         "copy stream, depth + 2 streams fit the process's 4 hardware queues at depth 2")
+    ap.add_argument("--host-depth", type=int, default=None,
+                    help="batches in flight of the host-input legs (make_to_tensor_fn(depth)): default 2 (with the "
+                         "cells' copy stream, depth + 2 streams fit the process's 4 hardware queues), 4 for "
+                         "progressive workloads (high-priority slot streams, DecodePipeline)")
     ap.add_argument("--host-reps", type=int, default=3,
                     help="back-to-back runs of the copying host-input leg (value_host_input = their median)")
     ap.add_argument("--dataset-copy", action="store_true",
                     help="dataset legs through the copying to_tensor_fn instead of registering the mapped "
                          "fragments' image buffers")
     args = ap.parse_args()
+    progressive = args.workload.endswith("p")
+    if args.depth is None:
+        args.depth = 4 if progressive else 3
+    if args.host_depth is None:
+        args.host_depth = 4 if progressive else 2
 
     import numpy as np
     import torch

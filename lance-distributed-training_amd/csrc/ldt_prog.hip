@@ -31,8 +31,14 @@ namespace ldt {
 
 namespace {
 
-constexpr int kWin = 4096;  // scan bytes staged in LDS (per wave)
-constexpr int kChunk = 32;  // blocks staged per round (one per lane)
+#ifndef LDT_PROG_WIN
+#define LDT_PROG_WIN 1024
+#endif
+#ifndef LDT_PROG_CHUNK
+#define LDT_PROG_CHUNK 32
+#endif
+constexpr int kWin = LDT_PROG_WIN;     // scan bytes staged in LDS (per wave)
+constexpr int kChunk = LDT_PROG_CHUNK; // blocks staged per round (one per lane)
 constexpr int kWaves = 4;   // scans of one chain in flight (one wave each)
 
 struct ProgLds {
@@ -45,20 +51,43 @@ struct ProgLds {
   int64_t bidx[kChunk]; // coefficient-buffer block index of each staged slot
   uint64_t nzm[kChunk];  // AC refinement: zigzag positions nonzero before the scan
   uint64_t corr[kChunk]; // AC refinement: positions whose correction bit is 1
-  ProgTab tabs[4];
-  int64_t win_base, win_lim; // data offsets of win[0] and one past its last valid byte
-  int64_t pos;               // lane 0's reader position (for window refills)
+  uint64_t newm[kChunk]; // AC refinement: positions given a new value (+-1 << Al)
+  uint64_t negm[kChunk]; // AC refinement: ... of which the negative ones
+  int win_base, win_lim; // scan offsets of win[0] and one past its last valid byte
+  int pos;               // the reader position (for window refills)
+};
+// The DC chain runs on wave 0 alone; its Huffman tables (one per component of
+// an interleaved DC scan) live in the LDS of the idle waves 1..3.
+static_assert(sizeof(ProgLds) * 3 >= sizeof(ProgTab) * 4, "DC tables do not fit");
+
+// An AC scan's Huffman table held in the wave's registers (all 64 lanes hold a
+// piece), so a symbol decode makes no LDS access:
+//   lane l in 1..16: lim = (maxcode[l] + 1) << (16 - l), the 16-bit
+//   left-aligned limit of the length-l codes (0 when there are none), and
+//   voff = valoffset[l];
+//   every lane: 4 of the 256 symbol bytes.
+// jdhuff.c jpeg_huff_decode's search (the smallest l with code <= maxcode[l])
+// is the smallest l with peek16 < lim[l]: one compare across the lanes, a
+// ballot and a find-first-set, then two readlanes for the symbol.
+struct RegTab {
+  uint32_t lim;
+  int32_t voff;
+  uint32_t vals;
 };
 
-// Lane 0's bit reader: jdhuff.c semantics (MSB first, FF00 -> FF, FF fill
-// bytes skipped, zero bits once a marker is reached).
+// The wave's bit reader: jdhuff.c semantics (MSB first, FF00 -> FF, FF fill
+// bytes skipped, zero bits once a marker is reached). Offsets are relative to
+// the scan's first entropy-coded byte (the planner keeps scans below 2 GB).
 struct PReader {
   const uint8_t *data;
-  int64_t pos, lim; // lim: one past the marker that ends the scan
-  int64_t wb, wl;   // the LDS window's data range (copied from ProgLds)
+  int pos, lim; // lim: one past the marker that ends the scan
+  int wb, wl;   // the LDS window's scan range (copied from ProgLds)
   uint64_t buf;
   int bits;
   int marker; // 0: none yet; else the marker code reached
+#ifdef LDT_PROG_STATS
+  int n_sym, n_corr, n_fill, n_slow; // diagnostic counts (see k_prog)
+#endif
 };
 
 // The whole wave runs the decoder with identical values; every value read
@@ -70,9 +99,9 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
 }
 
-__device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int64_t p) {
+__device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int p) {
   int v;
-  if (p < r.wl) v = L.win[(int)(p - r.wb)];
+  if (p < r.wl) v = L.win[p - r.wb];
   else v = __builtin_nontemporal_load(r.data + p);
   return (int)uni((uint32_t)v);
 }
@@ -80,9 +109,15 @@ __device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int64_t
 // Appends whole bytes while at most 56 bits are buffered. Fast path: the next
 // 8 window bytes hold no 0xFF (no stuffing, no marker) -> one read of three
 // aligned LDS words instead of a dependent read per byte.
+#ifdef LDT_PROG_STATS
+#define PCNT(r, f, v) ((r).f += (v))
+#else
+#define PCNT(r, f, v)
+#endif
 __device__ __forceinline__ void pfill(PReader &r, const ProgLds &L) {
+  PCNT(r, n_fill, 1);
   if (r.marker == 0 && r.pos + 12 <= r.wl) {
-    const int o = (int)(r.pos - r.wb);
+    const int o = r.pos - r.wb;
     const uint32_t a = uni(L.win32[o >> 2]), b = uni(L.win32[(o >> 2) + 1]),
                    c = uni(L.win32[(o >> 2) + 2]);
     const uint32_t sh = (uint32_t)(o & 3) * 8;
@@ -103,6 +138,7 @@ __device__ __forceinline__ void pfill(PReader &r, const ProgLds &L) {
       return;
     }
   }
+  PCNT(r, n_slow, 1);
   while (r.bits <= 56) {
     int c = 0;
     if (r.marker == 0 && r.pos < r.lim) {
@@ -134,7 +170,8 @@ __device__ __forceinline__ int pget(PReader &r, const ProgLds &L, int n) {
   return v;
 }
 
-// jdhuff.c jpeg_huff_decode: 8-bit lookahead, then the canonical search.
+// jdhuff.c jpeg_huff_decode on an LDS table (DC scans): 8-bit lookahead, then
+// the canonical search.
 __device__ __forceinline__ int phuff(PReader &r, const ProgLds &L, const ProgTab &t) {
   if (r.bits < 16) pfill(r, L);
   const uint32_t e = uni(t.look[r.buf >> 56]);
@@ -156,6 +193,55 @@ __device__ __forceinline__ int phuff(PReader &r, const ProgLds &L, const ProgTab
   r.buf <<= 16; // corrupt data: libjpeg warns and returns symbol 0
   r.bits -= 16;
   return 0;
+}
+
+// Lane 17 matches every peek (lim = all ones): the ballot is never empty,
+// and l = 17 stands for a code no table entry matches (libjpeg: warning,
+// symbol 0, 16 bits consumed). For a refinement scan the symbol bytes are
+// stored as classes: r | 0x10 when the size is nonzero (a sign bit follows) |
+// 0x20 for EOBr (size 0, r < 15), so the decoder tests bits instead of
+// comparing r and the size; corrupt codes then read as 0x20 (EOB0).
+__device__ __forceinline__ RegTab reg_tab(const ProgTab &t, int lane, bool refine) {
+  RegTab r;
+  const bool has = lane >= 1 && lane <= 16;
+  const int mc = has ? t.maxcode[lane] : -1;
+  r.lim = lane == 17 ? ~0u : (mc < 0 ? 0u : (uint32_t)(mc + 1) << (16 - lane));
+  r.voff = has ? t.valoff[lane] : 0;
+  uint32_t v = reinterpret_cast<const uint32_t *>(t.vals)[lane];
+  if (refine) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t sym = (v >> (8 * b)) & 0xFF, rr = sym >> 4, sz = sym & 15;
+      const uint32_t cls = rr | (sz ? 0x10u : 0u) | (sz == 0 && rr != 15 ? 0x20u : 0u);
+      c |= cls << (8 * b);
+    }
+    v = c;
+  }
+  r.vals = v;
+  return r;
+}
+
+// The symbol (or class) at the front of the buffer, which holds at least 16
+// bits (the caller has filled it); consumes its code. Branch-free: a ballot
+// of peek16 < lim[l] over the lanes, its lowest lane l, two readlanes.
+__device__ __forceinline__ int sym_reg(PReader &r, const RegTab &t, int corrupt_sym) {
+  PCNT(r, n_sym, 1);
+  const uint32_t w = (uint32_t)(r.buf >> 48);
+  const uint64_t hit = __builtin_amdgcn_ballot_w64(w < t.lim);
+  const int l = (int)__builtin_ctzll(hit); // 1..17 (lane 17 always matches)
+  const int len = min(l, 16);
+  const int idx = __builtin_amdgcn_readlane(t.voff, l) + (int)(w >> (16 - len));
+  const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)t.vals, (idx >> 2) & 63);
+  const int sym = (int)((word >> ((idx & 3) * 8)) & 0xFF);
+  r.buf <<= len;
+  r.bits -= len;
+  return l > 16 ? corrupt_sym : sym;
+}
+
+// Lane i's count of the set bits of m below bit i.
+__device__ __forceinline__ uint32_t rank_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 __device__ __forceinline__ int pextend(int v, int s) {
@@ -182,32 +268,173 @@ __device__ __forceinline__ void prestart(PReader &r, const ProgLds &L) {
   }
 }
 
-// AC refinement correction bits for the already-nonzero positions in `seg`
-// (ascending zigzag order, one bit each, read 16 at a time): returns the
-// positions whose bit is 1. The corrections themselves (jdphuff.c: c += p1 or
-// m1 when (c & p1) == 0) are applied lane-parallel after the chunk.
-__device__ __forceinline__ uint64_t pcorr(PReader &r, const ProgLds &L, uint64_t seg) {
-  uint64_t res = 0;
-  while (seg) {
-    const int cnt = min(__popcll(seg), 16);
-    const int bits = pget(r, L, cnt);
-    for (int j = cnt - 1; j >= 0; --j) {
-      const uint64_t low = seg & (0ull - seg);
-      res |= ((bits >> j) & 1) ? low : 0ull;
-      seg ^= low;
-    }
-  }
-  return res;
-}
-
 __device__ __forceinline__ uint64_t mask_from(int k) { return k >= 64 ? 0ull : (~0ull << k); }
 __device__ __forceinline__ uint64_t mask_below(int k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
 
+// jdphuff.c process_restart's caller side: every `restart` units the reader
+// drops its bits and consumes RSTn; the DC predictors and the EOB run reset.
+__device__ __forceinline__ bool restart_due(PReader &R, const ProgLds &L, int restart, int &togo) {
+  if (!restart) return false;
+  bool did = false;
+  if (togo == 0) {
+    prestart(R, L);
+    togo = restart;
+    did = true;
+  }
+  --togo;
+  return did;
+}
+
+// decode_mcu_AC_first over the chunk's nu blocks (single-component scan).
+// EOBr is size 0 with r < 15, i.e. ((c + 0x10) & 0x10F) == 0; ZRL (r = 15,
+// size 0) advances k by 16 like a value of size 0 that is not stored.
+__device__ __forceinline__ void ac_first_chunk(PReader &R, ProgLds &L, const RegTab &rt, int nu, int Ss, int Se,
+                                               int Al, int &eobrun, int &togo, int restart, bool w0) {
+  for (int slot = 0; slot < nu; ++slot) {
+    if (restart_due(R, L, restart, togo)) eobrun = 0;
+    if (eobrun > 0) {
+      --eobrun;
+      continue;
+    }
+    int16_t *blk = L.blk[slot];
+    for (int k = Ss; k <= Se; ++k) {
+      if (R.bits < 32) pfill(R, L); // the code (<= 16 bits) and its value bits (<= 15)
+      const int c = sym_reg(R, rt, 0);
+      if (((c + 0x10) & 0x10F) == 0) { // EOBr
+        const int r = c >> 4;
+        eobrun = 1 << r;
+        if (r) eobrun += pget(R, L, r);
+        --eobrun;
+        break;
+      }
+      const int t = c & 15;
+      k += c >> 4;
+      if (t) {
+        const int v = pextend((int)(R.buf >> (64 - t)), t) * (1 << Al);
+        R.buf <<= t;
+        R.bits -= t;
+        if (w0) blk[min(k, 63)] = (int16_t)v;
+      }
+    }
+  }
+}
+
+// decode_mcu_AC_refine over the chunk's nu blocks, on bit masks. jdphuff.c
+// walks k one coefficient at a time: a nonzero (history) coefficient takes a
+// correction bit, the (r+1)-th zero stops the walk and receives the new value.
+// Here the walk is indexed by zero rank: per block the lanes tabulate, for
+// each rank q, the band's q-th zero position P(q) and the count C(q) of
+// history nonzeros below it (one forward permute), so a symbol with run r
+// moves the rank q by r + 1, reads its stop P(q) with one readlane, and takes
+// C(q) - C(previous stop) correction bits. The correction bits (which are in
+// position order over the block), the ranks given a new value and the sign
+// bits are accumulated in SGPRs and deposited on the lanes at the block's end
+// as the position masks corr / newm / negm; lane 0 stores them and the lanes
+// apply them after the chunk (corrections first, then the new values, the
+// order jdphuff.c's walk gives).
+__device__ __forceinline__ uint64_t pget64(PReader &r, const ProgLds &L, int n) {
+  if (n <= 32) return (uint32_t)pget(r, L, n);
+  const uint64_t hi = (uint32_t)pget(r, L, n - 32);
+  return (hi << 32) | (uint32_t)pget(r, L, 32);
+}
+
+__device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const RegTab &rt, int nu, int Ss, int Se,
+                                                int &eobrun, int &togo, int restart, bool w0) {
+  const int lane = (int)(threadIdx.x & 63);
+  const uint64_t band = mask_from(Ss) & mask_below(Se + 1);
+  for (int slot = 0; slot < nu; ++slot) {
+    if (restart_due(R, L, restart, togo)) eobrun = 0;
+    const uint64_t nzh = uni64(L.nzm[slot]);
+    const uint64_t N = nzh & band;  // history nonzeros of the band
+    const uint64_t Z = ~nzh & band; // positions of the band still zero
+    const int ntot = __popcll(N);
+    const int nz0 = __popcll(Z);
+    const uint32_t jz = rank_below(Z), jn = rank_below(N);
+    const bool in_z = (Z >> lane) & 1;
+    int ccons = 0;        // corrections read: the first ccons nonzeros of N
+    uint64_t cbits = 0;   // their bits, the first read most significant
+    uint64_t rmask = 0;   // zero ranks that received a new value
+    uint64_t sbits = 0;   // the new values' sign bits, the first read most significant
+    int nsgn = 0;
+    int ovf = -1;         // a value placed past the band's last zero (jdphuff.c
+                          // natural_order[Se + 1]; corrupt data only)
+    if (eobrun == 0) {
+      // lane q <- (P(q) | C(q) << 8); ranks q >= nz0: (Se + 1, ntot). Each lane
+      // sends to a distinct rank: zero positions to their rank, the others to
+      // nz0 + their rank among the non-zero positions.
+      const uint32_t dst = in_z ? jz : (uint32_t)nz0 + ((uint32_t)lane - jz);
+      const uint32_t val = in_z ? ((uint32_t)lane | (jn << 8)) : ((uint32_t)(Se + 1) | ((uint32_t)ntot << 8));
+      const int pc = __builtin_amdgcn_ds_permute((int)(dst * 4), (int)val);
+      int rn = 0; // the rank of the next zero
+      while (true) {
+        if (R.bits < 17) pfill(R, L); // the code (<= 16 bits) and the sign bit
+        const int c = sym_reg(R, rt, 0x20);
+        if (c & 0x20) { // EOBr
+          const int r = c & 15;
+          eobrun = 1 << r;
+          if (r) eobrun += pget(R, L, r);
+          break;
+        }
+        // a nonzero size takes a sign bit (1: +p1)
+        const int t1 = (c >> 4) & 1;
+        sbits = (sbits << t1) | ((R.buf >> 63) & (uint64_t)t1);
+        R.buf <<= t1;
+        R.bits -= t1;
+        nsgn += t1;
+        const int q = rn + (c & 15); // the stop's zero rank (ZRL: the 16th zero)
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(pc, min(q, 63));
+        const int stop = (int)(e & 0xFF);
+        int nc = (int)(e >> 8) - ccons; // nonzeros passed: one correction bit each
+        ccons += nc;
+        PCNT(R, n_corr, nc);
+        if (nc > 32) {
+          cbits = (cbits << 32) | (uint32_t)pget(R, L, 32);
+          nc -= 32;
+        }
+        if (nc > R.bits) pfill(R, L);
+        const uint64_t cv = nc ? (R.buf >> (64 - nc)) : 0ull;
+        cbits = (cbits << nc) | cv;
+        R.buf <<= nc;
+        R.bits -= nc;
+        const bool inr = q < nz0;
+        rmask |= (uint64_t)(t1 & (int)inr) << (q & 63);
+        ovf = (t1 && !inr) ? min(stop, 63) : ovf;
+        rn = q + 1;
+        if (stop >= Se) break; // the walk's next k is past Se
+      }
+    }
+    if (eobrun > 0) { // the rest of the band's nonzeros take correction bits
+      const int nc = ntot - ccons;
+      if (nc) {
+        cbits = (cbits << nc) | pget64(R, L, nc);
+        ccons = ntot;
+      }
+      --eobrun;
+    }
+    // deposit on the positions (lane j = zigzag position j)
+    const bool in_n = (N >> lane) & 1;
+    const bool cb = in_n && (int)jn < ccons && ((cbits >> (((uint32_t)ccons - 1u - jn) & 63u)) & 1);
+    const uint64_t corr = __builtin_amdgcn_ballot_w64(cb);
+    uint64_t newm = __builtin_amdgcn_ballot_w64(in_z && ((rmask >> (jz & 63u)) & 1));
+    if (ovf >= 0) newm |= 1ull << ovf;
+    const uint32_t jw = rank_below(newm);
+    const bool in_w = (newm >> lane) & 1;
+    const uint64_t negm =
+        __builtin_amdgcn_ballot_w64(in_w && !((sbits >> (((uint32_t)nsgn - 1u - jw) & 63u)) & 1));
+    if (w0) {
+      L.corr[slot] = corr;
+      L.newm[slot] = newm;
+      L.negm[slot] = negm;
+    }
+  }
+}
+
 // Stage scan bytes [base, min(base + kWin, lim)) into the window (all lanes).
-__device__ void load_window(ProgLds &L, const uint8_t *data, int64_t base, int64_t lim) {
+__device__ void load_window(ProgLds &L, const uint8_t *data, int base, int lim) {
   const int lane = threadIdx.x & 63;
-  const int64_t n = min((int64_t)kWin, lim - base);
-  for (int64_t o = lane; o < n; o += 64) L.win[o] = data[base + o];
+  const int n = min(kWin, lim - base);
+#pragma unroll 1
+  for (int o = lane; o < n; o += 64) L.win[o] = data[base + o];
   if (lane == 0) {
     L.win_base = base;
     L.win_lim = base + n;
@@ -223,14 +450,28 @@ __device__ __forceinline__ void wave_sync() {
 
 } // namespace
 
-__global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict__ descs,
+// Diagnostic build (-DLDT_PROG_STATS): the luma AC chain's time split, summed
+// over images in 10 ns ticks into the plan's debug counters (dbg[jc]: scan jc
+// from start to end; dbg[4 + jc]: waiting for scan jc-1; dbg[8 + jc]: entropy
+// decode; dbg[12..14]: the last scan's Huffman symbols, correction bits and
+// buffer fills; dbg[15]: luma chains).
+#ifdef LDT_PROG_STATS
+#define PSTAT_T(v) const uint64_t v = wall_clock64()
+#define PSTAT_ADD(i, t0) \
+  if (stat && w0) atomicAdd(dbg + (i), (int)(wall_clock64() - (t0)))
+#else
+#define PSTAT_T(v)
+#define PSTAT_ADD(i, t0)
+#endif
+
+__global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restrict__ descs,
                                              const int32_t *__restrict__ prog_img,
                                              const ProgScan *__restrict__ scans,
                                              const ProgTab *__restrict__ ptabs,
                                              const uint8_t *__restrict__ data,
                                              int16_t *__restrict__ pcoef,
                                              int16_t *__restrict__ dcv,
-                                             const int32_t *__restrict__ status) {
+                                             const int32_t *__restrict__ status, int32_t *dbg) {
   __shared__ ProgLds Lw[kWaves];
   __shared__ int progress[kMaxProgScans]; // chunks of each chain scan written back
   // chain 0: the DC scans (dcv only); chain 1 + c: component c's AC scans
@@ -256,6 +497,7 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
   const int lane = (int)(threadIdx.x & 63);
   if (chain == 0 && wave != 0) return;
   ProgLds &L = Lw[wave];
+  ProgTab *dctabs = reinterpret_cast<ProgTab *>(&Lw[1]); // DC chain only
   const int64_t nblk = (int64_t)d.mcux * d.mcuy * d.bpm;
   // DC values start at zero: blocks no DC scan covers (the padding blocks of
   // non-interleaved DC scans) must not keep an earlier batch's value
@@ -268,9 +510,11 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
     for (int b = d.bpm - 1; b >= 0; --b)
       if (d.bcomp[b] == c) b0[c] = b;
   }
-  PReader R;
-  R.data = data;
-  int pred[4] = {0, 0, 0, 0};
+  const bool w0 = lane == 0; // the lane that stores
+#ifdef LDT_PROG_STATS
+  const bool stat = dbg != nullptr && chain == 1;
+  if (stat && w0 && wave == 0) atomicAdd(dbg + 15, 1);
+#endif
   int jc = -1; // index of the scan within the chain
   for (int si = 0; si < d.prog_count; ++si) {
     const ProgScan &sc = scans[d.prog_first + si];
@@ -281,15 +525,25 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
     const bool piped = chain != 0;
     if (piped && jc % kWaves != wave) continue; // another wave's scan
     const bool wait_prev = piped && jc > 0;
+    PSTAT_T(t_scan0);
+    const int js = min(jc, 3);
+    (void)js;
     wave_sync();
-    for (int k = 0; k < 4; ++k) {
-      if (sc.tab[k] < 0) continue;
-      const uint32_t *src = reinterpret_cast<const uint32_t *>(ptabs + sc.tab[k]);
-      uint32_t *dst = reinterpret_cast<uint32_t *>(&L.tabs[k]);
-      for (int o = lane; o < (int)(sizeof(ProgTab) / 4); o += 64) dst[o] = src[o];
+    RegTab rt = {0u, 0, 0u};
+    if (dcband) {
+      for (int k = 0; k < 4; ++k) {
+        if (sc.tab[k] < 0) continue;
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(ptabs + sc.tab[k]);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(&dctabs[k]);
+        for (int o = lane; o < (int)(sizeof(ProgTab) / 4); o += 64) dst[o] = src[o];
+      }
+    } else {
+      rt = reg_tab(ptabs[sc.tab[0]], lane, Ah != 0);
     }
-    const int64_t lim = sc.data_off + sc.data_len + 2; // through the ending marker
-    load_window(L, data, sc.data_off, lim);
+    PReader R;
+    R.data = data + sc.data_off;
+    R.lim = (int)sc.data_len + 2; // through the ending marker
+    load_window(L, R.data, 0, R.lim);
     wave_sync();
     // units: MCUs of the interleaved grid, or the component's own blocks
     int ux, uy, bpu = 0;
@@ -309,21 +563,25 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
     }
     const int64_t units = (int64_t)ux * uy;
     const int upc = kChunk / bpu;
-    R.pos = sc.data_off;
-    R.lim = lim;
+    R.pos = 0;
     R.buf = 0;
     R.bits = 0;
     R.marker = 0;
-    pred[0] = pred[1] = pred[2] = pred[3] = 0;
-    int64_t eobrun = 0;
+#ifdef LDT_PROG_STATS
+    R.n_sym = R.n_corr = R.n_fill = R.n_slow = 0;
+#endif
+    int pred[4] = {0, 0, 0, 0};
+    int eobrun = 0;
     int togo = sc.restart;
     const int p1 = 1 << Al, m1 = -(1 << Al);
     for (int64_t u0 = 0, ci = 0; u0 < units; u0 += upc, ++ci) {
       const int nu = (int)min((int64_t)upc, units - u0);
       const int nbk = nu * bpu;
+      PSTAT_T(t_w0);
       if (wait_prev) // scan jc-1 has written this chunk back
         while (__hip_atomic_load(&progress[jc - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= ci)
           __builtin_amdgcn_s_sleep(1);
+      PSTAT_ADD(4 + js, t_w0);
       // stage the chunk's blocks: lane j -> block j of the chunk, scan order
       if (lane < nbk) {
         const int64_t u = u0 + lane / bpu;
@@ -361,109 +619,52 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
             }
           }
           L.nzm[lane] = nz;
-          L.corr[lane] = 0;
         }
       }
       wave_sync();
-      const bool w0 = lane == 0; // the lane that stores
-      {
-        R.wb = (int64_t)uni64((uint64_t)L.win_base);
-        R.wl = (int64_t)uni64((uint64_t)L.win_lim);
+
+      PSTAT_T(t_dec0);
+      R.wb = (int)uni((uint32_t)L.win_base);
+      R.wl = (int)uni((uint32_t)L.win_lim);
+      if (!dcband) {
+        if (Ah == 0)
+          ac_first_chunk(R, L, rt, nu, Ss, Se, Al, eobrun, togo, sc.restart, w0);
+        else
+          ac_refine_chunk(R, L, rt, nu, Ss, Se, eobrun, togo, sc.restart, w0);
+      } else {
         int slot = 0;
         for (int ui = 0; ui < nu; ++ui) {
-          if (sc.restart) {
-            if (togo == 0) {
-              prestart(R, L);
-              pred[0] = pred[1] = pred[2] = pred[3] = 0;
-              eobrun = 0;
-              togo = sc.restart;
-            }
-            --togo;
-          }
+          if (restart_due(R, L, sc.restart, togo)) pred[0] = pred[1] = pred[2] = pred[3] = 0;
           for (int i = 0; i < ns; ++i) {
             const int nb = ns == 1 ? 1 : d.ch[sc.comp[i]] * d.cv[sc.comp[i]];
             for (int q = 0; q < nb; ++q, ++slot) {
-              if (dcband && Ah == 0) { // decode_mcu_DC_first
-                const int t = phuff(R, L, L.tabs[i]);
+              if (Ah == 0) { // decode_mcu_DC_first
+                const int t = phuff(R, L, dctabs[i]);
                 pred[i] += pextend(pget(R, L, t), t);
                 if (w0) L.dc[slot] = (int16_t)(pred[i] * (1 << Al));
-              } else if (dcband) { // decode_mcu_DC_refine
+              } else { // decode_mcu_DC_refine
                 if (pget(R, L, 1) && w0) L.dc[slot] = (int16_t)(L.dc[slot] | p1);
-              } else if (Ah == 0) { // decode_mcu_AC_first
-                if (eobrun > 0) {
-                  --eobrun;
-                  continue;
-                }
-                int16_t *blk = L.blk[slot];
-                for (int k = Ss; k <= Se; ++k) {
-                  const int rs = phuff(R, L, L.tabs[0]);
-                  const int r = rs >> 4, t = rs & 15;
-                  if (t) {
-                    k += r;
-                    const int v = pextend(pget(R, L, t), t) * (1 << Al);
-                    if (w0) blk[min(k, 63)] = (int16_t)v;
-                  } else if (r == 15) {
-                    k += 15;
-                  } else {
-                    eobrun = (int64_t)1 << r;
-                    if (r) eobrun += pget(R, L, r);
-                    --eobrun;
-                    break;
-                  }
-                }
-              } else { // decode_mcu_AC_refine, on bit masks of the block
-                // jdphuff.c walks k one coefficient at a time: a nonzero
-                // (history) coefficient takes a correction bit, the (r+1)-th
-                // zero stops the walk and receives the new value. Here the
-                // history is the 64-bit mask nzh, the stop is found by
-                // clearing r zero bits, and the correction bits of the
-                // nonzeros passed are read in bulk (pcorr).
-                int16_t *blk = L.blk[slot];
-                const uint64_t nzh = uni64(L.nzm[slot]);
-                const uint64_t band = mask_below(Se + 1);
-                uint64_t corr = 0;
-                int k = Ss;
-                if (eobrun == 0) {
-                  for (; k <= Se; ++k) {
-                    const int rs = phuff(R, L, L.tabs[0]);
-                    const int r = rs >> 4;
-                    const int t = rs & 15;
-                    int sv = 0;
-                    if (t) {
-                      sv = pget(R, L, 1) ? p1 : m1;
-                    } else if (r != 15) {
-                      eobrun = (int64_t)1 << r;
-                      if (r) eobrun += pget(R, L, r);
-                      break;
-                    }
-                    uint64_t z = ~nzh & mask_from(k) & band;
-                    for (int q = 0; q < r && z; ++q) z &= z - 1;
-                    const int stop = z ? __ffsll((unsigned long long)z) - 1 : Se + 1;
-                    corr |= pcorr(R, L, nzh & mask_from(k) & mask_below(stop));
-                    k = stop;
-                    if (sv && w0) blk[min(k, 63)] = (int16_t)sv;
-                  }
-                }
-                if (eobrun > 0) {
-                  corr |= pcorr(R, L, nzh & mask_from(k) & band);
-                  --eobrun;
-                }
-                if (w0) L.corr[slot] = corr;
               }
             }
           }
         }
-        if (w0) L.pos = R.pos;
       }
+      if (w0) L.pos = R.pos;
       wave_sync();
+      PSTAT_ADD(8 + js, t_dec0);
       if (lane < nbk) {
         const int64_t gb = L.bidx[lane];
-        if (!dcband && Ah != 0) { // apply this block's refinement corrections
+        if (!dcband && Ah != 0) { // apply this block's refinement: corrections, then new values
           int16_t *blk = L.blk[lane];
           for (uint64_t cm = L.corr[lane]; cm; cm &= cm - 1) {
             const int pos = __ffsll((unsigned long long)cm) - 1;
             const int c = blk[pos];
             if ((c & p1) == 0) blk[pos] = (int16_t)(c >= 0 ? c + p1 : c + m1);
+          }
+          const uint64_t ng = L.negm[lane];
+          for (uint64_t nm = L.newm[lane]; nm; nm &= nm - 1) {
+            const int pos = __ffsll((unsigned long long)nm) - 1;
+            blk[pos] = (int16_t)(((ng >> pos) & 1) ? m1 : p1);
           }
         }
         if (dcband) {
@@ -482,20 +683,30 @@ __global__ void __launch_bounds__(64 * kWaves) k_prog(const ImgDesc *__restrict_
       }
       // keep at least half a window of bytes ahead of the reader
       wave_sync();
-      const int64_t pos = L.pos;
-      if (pos - L.win_base > kWin / 2 && L.win_lim < lim) {
+
+      const int pos = L.pos;
+      if (pos - L.win_base > kWin / 2 && L.win_lim < R.lim) {
         wave_sync();
-        load_window(L, data, pos, lim);
+        load_window(L, R.data, pos, R.lim);
       }
       wave_sync();
+
     }
+    PSTAT_ADD(js, t_scan0);
+#ifdef LDT_PROG_STATS
+    if (stat && w0 && jc == 3) {
+      atomicAdd(dbg + 12, R.n_sym);
+      atomicAdd(dbg + 13, R.n_corr);
+      atomicAdd(dbg + 14, R.n_fill);
+    }
+#endif
   }
 }
 
 hipError_t launch_prog(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_prog == 0) return hipSuccess;
   hipLaunchKernelGGL(k_prog, dim3(4 * p.n_prog), dim3(64 * kWaves), 0, s, p.descs, p.prog_img, p.pscans, p.ptabs,
-                     w.data, w.pcoef, w.dcv, w.status);
+                     w.data, w.pcoef, w.dcv, w.status, p.redo);
   return hipGetLastError();
 }
 

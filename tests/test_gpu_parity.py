@@ -638,6 +638,66 @@ def test_progressive_config_sized_batch():
             _check(img[k], oracle.jpeg_to_tensor(b), f"rep{rep}[{k}]")
 
 
+def _scan_ranges(b):
+    """(start, end) of each scan's entropy-coded bytes (SOS header skipped,
+    up to the marker that ends the scan; RSTn markers stay inside)."""
+    out, i = [], 2
+    while i + 4 <= len(b) and b[i] == 0xFF and b[i + 1] != 0xD9:
+        n = (b[i + 2] << 8) | b[i + 3]
+        if b[i + 1] != 0xDA:
+            i += 2 + n
+            continue
+        j = i + 2 + n
+        while not (b[j] == 0xFF and b[j + 1] != 0 and not 0xD0 <= b[j + 1] <= 0xD7):
+            j += 1
+        out.append((i + 2 + n, j))
+        i = j
+    return out
+
+
+@pytest.mark.parametrize("kind", ["420", "444"])
+def test_progressive_corrupt_scans_vs_oracle(kind):
+    """k_prog on damaged scans: bit flips inside the entropy-coded bytes of
+    randomly chosen scans (no new markers) drive the decoder through invalid
+    Huffman codes (16 bits skipped, symbol 0), overlong runs, EOB runs past the
+    band and refinement stops past Se. Whenever the batch decodes, the damaged
+    image equals the oracle's decode of the same bytes bit-exactly (libjpeg's
+    warn-and-continue semantics), and its clean neighbour is unaffected."""
+    import ldt_amd
+    from ldt_amd import synth
+
+    if kind == "420":
+        base = synth.encode(synth.field(512, 512, 11, 20.0), quality=90, progressive=True)
+    else:
+        base = synth.encode(synth.field(200, 264, 12, 30.0), quality=97, subsampling="4:4:4", progressive=True)
+    good = synth.encode(synth.field(96, 128, 13, 6.0), quality=80, progressive=True)
+    exp_good = oracle.jpeg_to_tensor(good)
+    scans = _scan_ranges(base)
+    assert len(scans) >= 6
+    rng = np.random.default_rng({"420": 21, "444": 22}[kind])
+    decoded = 0
+    for trial in range(16):
+        b = bytearray(base)
+        for _ in range(int(rng.integers(1, 4))):
+            s0, s1 = scans[int(rng.integers(len(scans)))]
+            for _ in range(20):
+                p = int(rng.integers(s0, s1))
+                v = b[p] ^ (1 << int(rng.integers(0, 8)))
+                if b[p] != 0xFF and v != 0xFF and b[p - 1] != 0xFF:
+                    b[p] = v
+                    break
+        cells = [bytes(b), good]
+        try:
+            out = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+        except ldt_amd.ImageDecodeError as e:
+            assert set(e.rows) == {0}, (kind, trial, e.rows)
+            continue
+        decoded += 1
+        _check(out[0], oracle.jpeg_to_tensor(bytes(b)), f"{kind} trial {trial}: damaged image")
+        _check(out[1], exp_good, f"{kind} trial {trial}: clean neighbour")
+    assert decoded >= 8, decoded
+
+
 def test_distributed_sampler_kernels_vs_torch_golden():
     """ldt_distributed_indices (MT19937 targets, deterministic-reservation
     Fisher-Yates, rank stride) vs torch's DistributedSampler: every golden case
