@@ -454,7 +454,8 @@ __device__ __forceinline__ void wave_sync() {
 // over images in 10 ns ticks into the plan's debug counters (dbg[jc]: scan jc
 // from start to end; dbg[4 + jc]: waiting for scan jc-1; dbg[8 + jc]: entropy
 // decode; dbg[12..14]: the last scan's Huffman symbols, correction bits and
-// buffer fills; dbg[15]: luma chains).
+// buffer fills; dbg[15]: luma chains). -DLDT_PROG_STATS=2: every chain's
+// scans, dbg[4 * chain + min(jc, 3)] = scan time (chain 0: the DC scans).
 #ifdef LDT_PROG_STATS
 #define PSTAT_T(v) const uint64_t v = wall_clock64()
 #define PSTAT_ADD(i, t0) \
@@ -512,8 +513,12 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
   }
   const bool w0 = lane == 0; // the lane that stores
 #ifdef LDT_PROG_STATS
+#if LDT_PROG_STATS == 2
+  const bool stat = dbg != nullptr;
+#else
   const bool stat = dbg != nullptr && chain == 1;
   if (stat && w0 && wave == 0) atomicAdd(dbg + 15, 1);
+#endif
 #endif
   int jc = -1; // index of the scan within the chain
   for (int si = 0; si < d.prog_count; ++si) {
@@ -563,6 +568,12 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
     }
     const int64_t units = (int64_t)ux * uy;
     const int upc = kChunk / bpu;
+    // the component (scan order) of each block of a unit, 2 bits per block
+    uint32_t cmap = 0;
+    for (int i = 0, b = 0; i < ns; ++i) {
+      const int nb = ns == 1 ? 1 : d.ch[sc.comp[i]] * d.cv[sc.comp[i]];
+      for (int q = 0; q < nb; ++q, ++b) cmap |= (uint32_t)i << (2 * b);
+    }
     R.pos = 0;
     R.buf = 0;
     R.bits = 0;
@@ -581,7 +592,9 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
       if (wait_prev) // scan jc-1 has written this chunk back
         while (__hip_atomic_load(&progress[jc - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= ci)
           __builtin_amdgcn_s_sleep(1);
+#if LDT_PROG_STATS != 2
       PSTAT_ADD(4 + js, t_w0);
+#endif
       // stage the chunk's blocks: lane j -> block j of the chunk, scan order
       if (lane < nbk) {
         const int64_t u = u0 + lane / bpu;
@@ -631,18 +644,24 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
           ac_first_chunk(R, L, rt, nu, Ss, Se, Al, eobrun, togo, sc.restart, w0);
         else
           ac_refine_chunk(R, L, rt, nu, Ss, Se, eobrun, togo, sc.restart, w0);
+      } else if (Ah != 0 && sc.restart == 0) {
+        // decode_mcu_DC_refine without restarts: one bit per block, in the
+        // chunk's block order, so the chunk's nbk (<= 32) bits are read at
+        // once and each lane takes its block's bit
+        const uint32_t bits = (uint32_t)pget(R, L, nbk);
+        if (lane < nbk && ((bits >> (nbk - 1 - lane)) & 1u)) L.dc[lane] = (int16_t)(L.dc[lane] | p1);
       } else {
         int slot = 0;
         for (int ui = 0; ui < nu; ++ui) {
           if (restart_due(R, L, sc.restart, togo)) pred[0] = pred[1] = pred[2] = pred[3] = 0;
-          for (int i = 0; i < ns; ++i) {
-            const int nb = ns == 1 ? 1 : d.ch[sc.comp[i]] * d.cv[sc.comp[i]];
-            for (int q = 0; q < nb; ++q, ++slot) {
-              if (Ah == 0) { // decode_mcu_DC_first
+          {
+            for (int b = 0; b < bpu; ++b, ++slot) {
+              const int i = (int)(cmap >> (2 * b)) & 3;
+              if (Ah == 0) { // decode_mcu_DC_first (size <= 15: the planner's check)
                 const int t = phuff(R, L, dctabs[i]);
                 pred[i] += pextend(pget(R, L, t), t);
                 if (w0) L.dc[slot] = (int16_t)(pred[i] * (1 << Al));
-              } else { // decode_mcu_DC_refine
+              } else { // decode_mcu_DC_refine (with restarts)
                 if (pget(R, L, 1) && w0) L.dc[slot] = (int16_t)(L.dc[slot] | p1);
               }
             }
@@ -651,7 +670,9 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
       }
       if (w0) L.pos = R.pos;
       wave_sync();
+#if LDT_PROG_STATS != 2
       PSTAT_ADD(8 + js, t_dec0);
+#endif
       if (lane < nbk) {
         const int64_t gb = L.bidx[lane];
         if (!dcband && Ah != 0) { // apply this block's refinement: corrections, then new values
@@ -692,8 +713,12 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
       wave_sync();
 
     }
+#if LDT_PROG_STATS == 2
+    PSTAT_ADD(4 * chain + js, t_scan0);
+#else
     PSTAT_ADD(js, t_scan0);
-#ifdef LDT_PROG_STATS
+#endif
+#if LDT_PROG_STATS == 1
     if (stat && w0 && jc == 3) {
       atomicAdd(dbg + 12, R.n_sym);
       atomicAdd(dbg + 13, R.n_corr);

@@ -25,3 +25,9 @@ for rep in range(2):
            "decode_us": [us(8 + i) for i in range(4)],
            "last_scan_per_image": {"symbols": int(out[12]) // nimg, "corr_bits": int(out[13]) // nimg,
                                    "fills": int(out[14]) // nimg}}, flush=True)
+
+if os.environ.get("LDT_PROG_STATS_MODE") == "2":
+    # library built with -DLDT_PROG_STATS=2: every chain's scan times
+    print("per image (us): chain 0 = DC scans, 1 = luma AC, 2/3 = chroma AC; scan order within the chain")
+    for ch in range(4):
+        print(ch, [round(float(out[4 * ch + j]) / n / 100.0, 1) for j in range(4)])
