@@ -587,13 +587,18 @@ class DecodePipeline:
         # = 0 / 1 forces either.
         q = _lib.hw_queues()
         env = os.environ.get("LDT_SLOT_PRIORITY")
-        self.high_priority = bool(int(env)) if env is not None else self.depth + 1 > q
-        copy_queues = self.depth if self.high_priority else self.depth + 2
-        if q < copy_queues:
+        if env is not None:
+            n_high = self.depth if int(env) else 0
+        else:  # up to q high-priority slots, the rest beside the consumer's stream
+            n_high = 0 if self.depth + 1 <= q else min(self.depth, q)
+        n_normal = self.depth - n_high
+        self.high_priority = n_high > 0
+        # the cells' DMA on the copy stream needs a normal queue of its own
+        if (n_normal + 2 > q) if n_normal else (n_high > q):
             for c in self.ctxs:
                 c.set_option(_lib.OPT_COPY_MODE, 1)
-        self.streams = [torch.cuda.Stream(self.dec.device, priority=-1 if self.high_priority else 0)
-                        for _ in range(self.depth)]
+        self.streams = [torch.cuda.Stream(self.dec.device, priority=-1 if i < n_high else 0)
+                        for i in range(self.depth)]
         self.pending = [deque() for _ in range(self.depth)]  # per slot: (ticket, n), oldest first
         self.last_ticket = None  # (slot, ticket) of the most recent decode
         self.k = 0

@@ -14,7 +14,7 @@ for v in "$@"; do
   for p in ${PRIOS:-0}; do
   for d in $D; do
     f=$O/${WL:-c2p}_${v}_q${q}_p${p}_d$d
-    LDT_SLOT_PRIORITY=$p GPU_MAX_HW_QUEUES=$q LDT_LIBRARY=$L timeout -k 10 300 python bench.py --workload ${WL:-c2p} --no-cpu-baseline --only-resident --depth $d --steps 60 > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
+    if [ "$p" = auto ]; then unset LDT_SLOT_PRIORITY; else export LDT_SLOT_PRIORITY=$p; fi; GPU_MAX_HW_QUEUES=$q LDT_LIBRARY=$L timeout -k 10 300 python bench.py --workload ${WL:-c2p} --no-cpu-baseline --only-resident --depth $d --steps 60 > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
     python3 -c "import json;d=json.load(open('$f.json'));print('${WL:-c2p} $v queues $q prio $p depth $d', d['value'], d['ms_per_step'])"
   done
   done
