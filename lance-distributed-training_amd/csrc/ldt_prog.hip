@@ -32,7 +32,7 @@ namespace ldt {
 namespace {
 
 #ifndef LDT_PROG_WIN
-#define LDT_PROG_WIN 1024
+#define LDT_PROG_WIN 512
 #endif
 #ifndef LDT_PROG_CHUNK
 #define LDT_PROG_CHUNK 32
@@ -49,10 +49,6 @@ struct ProgLds {
   __attribute__((aligned(16))) int16_t blk[kChunk][64]; // zigzag slots; [0] unused
   int16_t dc[kChunk];
   int64_t bidx[kChunk]; // coefficient-buffer block index of each staged slot
-  uint64_t nzm[kChunk];  // AC refinement: zigzag positions nonzero before the scan
-  uint64_t corr[kChunk]; // AC refinement: positions whose correction bit is 1
-  uint64_t newm[kChunk]; // AC refinement: positions given a new value (+-1 << Al)
-  uint64_t negm[kChunk]; // AC refinement: ... of which the negative ones
   int win_base, win_lim; // scan offsets of win[0] and one past its last valid byte
   int pos;               // the reader position (for window refills)
 };
@@ -338,13 +334,21 @@ __device__ __forceinline__ uint64_t pget64(PReader &r, const ProgLds &L, int n) 
   return (hi << 32) | (uint32_t)pget(r, L, 32);
 }
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+// nzv (lane j): block j's positions nonzero before the scan; corr_v / newm_v /
+// negm_v (lane j): block j's correction / new-value / negative masks out.
 __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const RegTab &rt, int nu, int Ss, int Se,
-                                                int &eobrun, int &togo, int restart, bool w0) {
+                                                int &eobrun, int &togo, int restart, uint64_t nzv,
+                                                uint64_t &corr_v, uint64_t &newm_v, uint64_t &negm_v) {
   const int lane = (int)(threadIdx.x & 63);
   const uint64_t band = mask_from(Ss) & mask_below(Se + 1);
   for (int slot = 0; slot < nu; ++slot) {
     if (restart_due(R, L, restart, togo)) eobrun = 0;
-    const uint64_t nzh = uni64(L.nzm[slot]);
+    const uint64_t nzh = readlane64(nzv, slot);
     const uint64_t N = nzh & band;  // history nonzeros of the band
     const uint64_t Z = ~nzh & band; // positions of the band still zero
     const int ntot = __popcll(N);
@@ -354,10 +358,9 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
     int ccons = 0;        // corrections read: the first ccons nonzeros of N
     uint64_t cbits = 0;   // their bits, the first read most significant
     uint64_t rmask = 0;   // zero ranks that received a new value
-    uint64_t sbits = 0;   // the new values' sign bits, the first read most significant
-    int nsgn = 0;
+    uint64_t smask = 0;   // ... of which positive (sign bit 1)
     int ovf = -1;         // a value placed past the band's last zero (jdphuff.c
-                          // natural_order[Se + 1]; corrupt data only)
+    int ovf_pos = 0;      // natural_order[Se + 1]; corrupt data only), its sign
     if (eobrun == 0) {
       // lane q <- (P(q) | C(q) << 8); ranks q >= nz0: (Se + 1, ntot). Each lane
       // sends to a distinct rank: zero positions to their rank, the others to
@@ -377,28 +380,32 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
         }
         // a nonzero size takes a sign bit (1: +p1)
         const int t1 = (c >> 4) & 1;
-        sbits = (sbits << t1) | ((R.buf >> 63) & (uint64_t)t1);
+        const int sgn = (int)(R.buf >> 63);
         R.buf <<= t1;
         R.bits -= t1;
-        nsgn += t1;
         const int q = rn + (c & 15); // the stop's zero rank (ZRL: the 16th zero)
         const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(pc, min(q, 63));
         const int stop = (int)(e & 0xFF);
         int nc = (int)(e >> 8) - ccons; // nonzeros passed: one correction bit each
         ccons += nc;
         PCNT(R, n_corr, nc);
-        if (nc > 32) {
-          cbits = (cbits << 32) | (uint32_t)pget(R, L, 32);
-          nc -= 32;
+        if (nc > R.bits) { // rare: more correction bits than the buffer holds
+          while (nc > 32) {
+            cbits = (cbits << 32) | (uint32_t)pget(R, L, 32);
+            nc -= 32;
+          }
+          if (nc > R.bits) pfill(R, L);
         }
-        if (nc > R.bits) pfill(R, L);
         const uint64_t cv = nc ? (R.buf >> (64 - nc)) : 0ull;
         cbits = (cbits << nc) | cv;
         R.buf <<= nc;
         R.bits -= nc;
         const bool inr = q < nz0;
-        rmask |= (uint64_t)(t1 & (int)inr) << (q & 63);
+        const uint64_t qb = (uint64_t)(t1 & (int)inr) << (q & 63);
+        rmask |= qb;
+        smask |= sgn ? qb : 0ull;
         ovf = (t1 && !inr) ? min(stop, 63) : ovf;
+        ovf_pos = (t1 && !inr) ? sgn : ovf_pos;
         rn = q + 1;
         if (stop >= Se) break; // the walk's next k is past Se
       }
@@ -416,15 +423,15 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
     const bool cb = in_n && (int)jn < ccons && ((cbits >> (((uint32_t)ccons - 1u - jn) & 63u)) & 1);
     const uint64_t corr = __builtin_amdgcn_ballot_w64(cb);
     uint64_t newm = __builtin_amdgcn_ballot_w64(in_z && ((rmask >> (jz & 63u)) & 1));
-    if (ovf >= 0) newm |= 1ull << ovf;
-    const uint32_t jw = rank_below(newm);
-    const bool in_w = (newm >> lane) & 1;
-    const uint64_t negm =
-        __builtin_amdgcn_ballot_w64(in_w && !((sbits >> (((uint32_t)nsgn - 1u - jw) & 63u)) & 1));
-    if (w0) {
-      L.corr[slot] = corr;
-      L.newm[slot] = newm;
-      L.negm[slot] = negm;
+    uint64_t negm = __builtin_amdgcn_ballot_w64(in_z && ((rmask >> (jz & 63u)) & 1) && !((smask >> (jz & 63u)) & 1));
+    if (ovf >= 0) {
+      newm |= 1ull << ovf;
+      negm = ovf_pos ? (negm & ~(1ull << ovf)) : (negm | (1ull << ovf));
+    }
+    if (lane == slot) {
+      corr_v = corr;
+      newm_v = newm;
+      negm_v = negm;
     }
   }
 }
@@ -596,6 +603,7 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
       PSTAT_ADD(4 + js, t_w0);
 #endif
       // stage the chunk's blocks: lane j -> block j of the chunk, scan order
+      uint64_t nzv = 0; // lane j: block j's nonzero positions (AC scans)
       if (lane < nbk) {
         const int64_t u = u0 + lane / bpu;
         int64_t blk;
@@ -631,19 +639,20 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
               nz |= (uint64_t)((w[h] >> 16) != 0) << (8 * q + 2 * h + 1);
             }
           }
-          L.nzm[lane] = nz;
+          nzv = nz;
         }
       }
       wave_sync();
 
       PSTAT_T(t_dec0);
+      uint64_t corr_v = 0, newm_v = 0, negm_v = 0;
       R.wb = (int)uni((uint32_t)L.win_base);
       R.wl = (int)uni((uint32_t)L.win_lim);
       if (!dcband) {
         if (Ah == 0)
           ac_first_chunk(R, L, rt, nu, Ss, Se, Al, eobrun, togo, sc.restart, w0);
         else
-          ac_refine_chunk(R, L, rt, nu, Ss, Se, eobrun, togo, sc.restart, w0);
+          ac_refine_chunk(R, L, rt, nu, Ss, Se, eobrun, togo, sc.restart, nzv, corr_v, newm_v, negm_v);
       } else if (Ah != 0 && sc.restart == 0) {
         // decode_mcu_DC_refine without restarts: one bit per block, in the
         // chunk's block order, so the chunk's nbk (<= 32) bits are read at
@@ -677,13 +686,13 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
         const int64_t gb = L.bidx[lane];
         if (!dcband && Ah != 0) { // apply this block's refinement: corrections, then new values
           int16_t *blk = L.blk[lane];
-          for (uint64_t cm = L.corr[lane]; cm; cm &= cm - 1) {
+          for (uint64_t cm = corr_v; cm; cm &= cm - 1) {
             const int pos = __ffsll((unsigned long long)cm) - 1;
             const int c = blk[pos];
             if ((c & p1) == 0) blk[pos] = (int16_t)(c >= 0 ? c + p1 : c + m1);
           }
-          const uint64_t ng = L.negm[lane];
-          for (uint64_t nm = L.newm[lane]; nm; nm &= nm - 1) {
+          const uint64_t ng = negm_v;
+          for (uint64_t nm = newm_v; nm; nm &= nm - 1) {
             const int pos = __ffsll((unsigned long long)nm) - 1;
             blk[pos] = (int16_t)(((ng >> pos) & 1) ? m1 : p1);
           }
