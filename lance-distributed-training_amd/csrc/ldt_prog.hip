@@ -440,8 +440,18 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
 __device__ void load_window(ProgLds &L, const uint8_t *data, int base, int lim) {
   const int lane = threadIdx.x & 63;
   const int n = min(kWin, lim - base);
-#pragma unroll 1
-  for (int o = lane; o < n; o += 64) L.win[o] = data[base + o];
+  // all loads in flight before the first LDS write (one memory latency per refill)
+  uint8_t v[kWin / 64];
+#pragma unroll
+  for (int i = 0; i < kWin / 64; ++i) {
+    const int o = lane + 64 * i;
+    v[i] = o < n ? data[base + o] : (uint8_t)0;
+  }
+#pragma unroll
+  for (int i = 0; i < kWin / 64; ++i) {
+    const int o = lane + 64 * i;
+    if (o < n) L.win[o] = v[i];
+  }
   if (lane == 0) {
     L.win_base = base;
     L.win_lim = base + n;
@@ -527,6 +537,11 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
   if (stat && w0 && wave == 0) atomicAdd(dbg + 15, 1);
 #endif
 #endif
+  int nchain = 0; // the chain's scans (the last one publishes no progress)
+  for (int si = 0; si < d.prog_count; ++si) {
+    const ProgScan &sc = scans[d.prog_first + si];
+    nchain += (sc.ss == 0 ? chain == 0 : chain == 1 + sc.comp[0]) ? 1 : 0;
+  }
   int jc = -1; // index of the scan within the chain
   for (int si = 0; si < d.prog_count; ++si) {
     const ProgScan &sc = scans[d.prog_first + si];
@@ -706,7 +721,7 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
             reinterpret_cast<int4 *>(pcoef + d.pcoef_off * 64)[coef_piece((int)(gb - d.coef_off), q, coef_npad(d))] = src[q];
         }
       }
-      if (piped) { // publish chunk ci once the wave's stores are done
+      if (piped && jc + 1 < nchain) { // publish chunk ci once the wave's stores are done
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0)
           __hip_atomic_store(&progress[jc], (int)(ci + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
