@@ -203,7 +203,7 @@ def main():
                     help="time without the per-stage HIP events (no roofline)")
     ap.add_argument("--depth", type=int, default=None,
                     help="batches in flight (ldt_amd.DecodePipeline: one context + HIP stream each); default 3, "
-                         "4 for progressive workloads (a c2p batch takes ~15 ms on the device)")
+                         "7 for progressive workloads (a c2p batch takes ~13 ms on the device)")
     ap.add_argument("--dataset-batches", type=int, default=12,
                     help="batches per rank of one epoch of the dataset leg (0: skip the leg)")
     ap.add_argument("--dataset-epochs", type=int, default=2,
@@ -219,7 +219,7 @@ def main():
                          "rocprofv3 --stats summary of the line's timed launches is taken from")
     ap.add_argument("--host-depth", type=int, default=None,
                     help="batches in flight of the host-input legs (make_to_tensor_fn(depth)): default 2 (with the "
-                         "cells' copy stream, depth + 2 streams fit the process's 4 hardware queues), 4 for "
+                         "cells' copy stream, depth + 2 streams fit the process's 4 hardware queues), 7 for "
                          "progressive workloads (high-priority slot streams, DecodePipeline)")
     ap.add_argument("--host-reps", type=int, default=3,
                     help="back-to-back runs of the copying host-input leg (value_host_input = their median)")
@@ -228,10 +228,12 @@ def main():
                          "fragments' image buffers")
     args = ap.parse_args()
     progressive = args.workload.endswith("p")
+    # progressive batches spend ~13 ms in k_prog: 7 in flight (4 slots on
+    # high-priority streams, 3 beside the consumer's; profiles/r4/prog_ab_r4.txt)
     if args.depth is None:
-        args.depth = 4 if progressive else 3
+        args.depth = 7 if progressive else 3
     if args.host_depth is None:
-        args.host_depth = 4 if progressive else 2
+        args.host_depth = 7 if progressive else 2
 
     import numpy as np
     import torch

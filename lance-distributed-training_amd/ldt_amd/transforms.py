@@ -593,8 +593,10 @@ class DecodePipeline:
             n_high = 0 if self.depth + 1 <= q else min(self.depth, q)
         n_normal = self.depth - n_high
         self.high_priority = n_high > 0
-        # the cells' DMA on the copy stream needs a normal queue of its own
-        if (n_normal + 2 > q) if n_normal else (n_high > q):
+        # the cells' DMA on the copy stream needs a normal queue of its own, and
+        # beside a mixed set of slots it measured slower (c2p depth 6: host
+        # input 35k vs 50k at depth 7 with the DMA on the slots' streams)
+        if (n_normal + 2 > q or n_high > 0) if n_normal else (n_high > q):
             for c in self.ctxs:
                 c.set_option(_lib.OPT_COPY_MODE, 1)
         self.streams = [torch.cuda.Stream(self.dec.device, priority=-1 if i < n_high else 0)
