@@ -31,6 +31,14 @@
 #include "ldt_device.hpp"
 #include "ldt_kernels.hpp"
 
+// The write pass's unit queue (see write_run): 2 units (the default: the
+// Huffman stage writes 166 MB per c2 batch instead of 235 MB unqueued, at the
+// same speed), 4 (-DLDT_EXP_WR_Q4: 132 MB, 2% slower c2) or none
+// (-DLDT_EXP_WR_Q1); profiles/r4/write_queue_ab_r4.txt.
+#if !defined(LDT_EXP_WR_Q1) && !defined(LDT_EXP_WR_Q4) && !defined(LDT_EXP_WR_NT)
+#define LDT_EXP_WR_Q2
+#endif
+
 namespace ldt {
 
 // LDS pointers keep their address space so loads compile to ds_read_* (a
@@ -398,6 +406,10 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
   int cg = -1;                       // its group index; < 0: none
 #if defined(LDT_EXP_WR_Q2)
   uint4 q2 = make_uint4(0u, 0u, 0u, 0u), q3 = q2;
+#elif defined(LDT_EXP_WR_Q4)
+  // a 4-unit queue: a run's units leave as whole 64-byte segments (a run
+  // starts at unit 8 x its first block, so unit 4i is 64-byte aligned)
+  uint4 q0 = make_uint4(0u, 0u, 0u, 0u), q1 = q0, q2 = q0;
 #endif
   uint32_t wu = (uint32_t)base * 8u; // units stored
   uint32_t gmask = 0;                // groups of the current block
@@ -427,6 +439,21 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
         coef_img[wu - 2] = q2;
         coef_img[wu - 1] = q3;
       }
+    }
+#elif defined(LDT_EXP_WR_Q4)
+    if (flush) { // q0..q2 hold the segment's units so far (a shift register)
+      if ((wu & 3u) == 3u) {
+        coef_img[wu - 3] = q0;
+        coef_img[wu - 2] = q1;
+        coef_img[wu - 1] = q2;
+        coef_img[wu] = cur;
+      } else {
+        q0 = q1;
+        q1 = q2;
+        q2 = cur;
+      }
+      gmask |= 1u << cg;
+      ++wu;
     }
 #else
     if (flush) {
@@ -466,13 +493,34 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
         coef_img[wu - 1] = q3;
       }
 #endif
+#if defined(LDT_EXP_WR_Q4)
+      if ((wu & 3u) == 3u) {
+        coef_img[wu - 3] = q0;
+        coef_img[wu - 2] = q1;
+        coef_img[wu - 1] = q2;
+        coef_img[wu] = cur;
+      } else {
+        q0 = q1;
+        q1 = q2;
+        q2 = cur;
+      }
+#else
       coef_img[wu] = cur;
+#endif
       gmask |= 1u << cg;
       ++wu;
     }
 #if defined(LDT_EXP_WR_Q2)
     else if (wu & 1u) {
       coef_img[wu - 1] = q3;
+    }
+#endif
+#if defined(LDT_EXP_WR_Q4)
+    { // the queue's pending units: the last n of q0..q2
+      const uint32_t n = wu & 3u, w0 = wu & ~3u;
+      if (n == 3u) coef_img[w0] = q0;
+      if (n >= 2u) coef_img[w0 + n - 2] = q1;
+      if (n >= 1u) coef_img[w0 + n - 1] = q2;
     }
 #endif
     rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
@@ -1246,7 +1294,13 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   return true;
 }
 
-__global__ void __launch_bounds__(kHuffThreads) k_huff_image(
+#if defined(LDT_EXP_WR_Q4) || defined(LDT_HUFF_WAVES4)
+// one 1024-lane workgroup per CU (its LDS): 4 waves per SIMD, up to 128 VGPRs
+#define LDT_HUFF_WPE __attribute__((amdgpu_waves_per_eu(4, 4)))
+#else
+#define LDT_HUFF_WPE
+#endif
+__global__ void __launch_bounds__(kHuffThreads) LDT_HUFF_WPE k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ data,
     const uint8_t *__restrict__ dstuf, const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
