@@ -355,12 +355,22 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
     const int nz0 = __popcll(Z);
     const uint32_t jz = rank_below(Z), jn = rank_below(N);
     const bool in_z = (Z >> lane) & 1;
+    // The walk's results collect on the lanes (VALU, off the scalar unit that
+    // the serial decode saturates): lane r = the band's r-th nonzero takes its
+    // correction bit (cbv), lane q = the q-th zero gets 1 | 2 * positive when a
+    // new value lands on it (rbv).
     int ccons = 0;        // corrections read: the first ccons nonzeros of N
-    uint64_t cbits = 0;   // their bits, the first read most significant
-    uint64_t rmask = 0;   // zero ranks that received a new value
-    uint64_t smask = 0;   // ... of which positive (sign bit 1)
+    uint32_t cbv = 0;
+    uint32_t rbv = 0;
     int ovf = -1;         // a value placed past the band's last zero (jdphuff.c
     int ovf_pos = 0;      // natural_order[Se + 1]; corrupt data only), its sign
+    // n (<= 32) correction bits, the first read most significant, for the
+    // nonzeros of ranks ccons .. ccons + n - 1
+    auto deposit = [&](uint32_t bits, int n) {
+      const uint32_t d = (uint32_t)lane - (uint32_t)ccons;
+      cbv = d < (uint32_t)n ? ((bits >> (((uint32_t)n - 1u - d) & 31u)) & 1u) : cbv;
+      ccons += n;
+    };
     if (eobrun == 0) {
       // lane q <- (P(q) | C(q) << 8); ranks q >= nz0: (Se + 1, ntot). Each lane
       // sends to a distinct rank: zero positions to their rank, the others to
@@ -387,43 +397,42 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
         const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(pc, min(q, 63));
         const int stop = (int)(e & 0xFF);
         int nc = (int)(e >> 8) - ccons; // nonzeros passed: one correction bit each
-        ccons += nc;
         PCNT(R, n_corr, nc);
-        if (nc > R.bits) { // rare: more correction bits than the buffer holds
+        if (nc > 32 || nc > R.bits) { // rare: long corrections or a low buffer
           while (nc > 32) {
-            cbits = (cbits << 32) | (uint32_t)pget(R, L, 32);
+            deposit((uint32_t)pget(R, L, 32), 32);
             nc -= 32;
           }
           if (nc > R.bits) pfill(R, L);
         }
-        const uint64_t cv = nc ? (R.buf >> (64 - nc)) : 0ull;
-        cbits = (cbits << nc) | cv;
+        const uint32_t cv = nc ? (uint32_t)(R.buf >> (64 - nc)) : 0u;
+        deposit(cv, nc);
         R.buf <<= nc;
         R.bits -= nc;
-        const bool inr = q < nz0;
-        const uint64_t qb = (uint64_t)(t1 & (int)inr) << (q & 63);
-        rmask |= qb;
-        smask |= sgn ? qb : 0ull;
-        ovf = (t1 && !inr) ? min(stop, 63) : ovf;
-        ovf_pos = (t1 && !inr) ? sgn : ovf_pos;
+        const int t1i = q < nz0 ? t1 : 0;
+        rbv = lane == q ? (uint32_t)(t1i | ((t1i & sgn) << 1)) : rbv;
+        ovf = (t1 && !t1i) ? min(stop, 63) : ovf;
+        ovf_pos = (t1 && !t1i) ? sgn : ovf_pos;
         rn = q + 1;
         if (stop >= Se) break; // the walk's next k is past Se
       }
     }
     if (eobrun > 0) { // the rest of the band's nonzeros take correction bits
-      const int nc = ntot - ccons;
-      if (nc) {
-        cbits = (cbits << nc) | pget64(R, L, nc);
-        ccons = ntot;
+      int nc = ntot - ccons;
+      while (nc > 32) {
+        deposit((uint32_t)pget(R, L, 32), 32);
+        nc -= 32;
       }
+      if (nc) deposit((uint32_t)pget(R, L, nc), nc);
       --eobrun;
     }
-    // deposit on the positions (lane j = zigzag position j)
+    // to the positions (lane j = zigzag position j): gather by rank
+    const uint32_t cb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(jn * 4u), (int)cbv);
+    const uint32_t rb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((jz & 63u) * 4u), (int)rbv);
     const bool in_n = (N >> lane) & 1;
-    const bool cb = in_n && (int)jn < ccons && ((cbits >> (((uint32_t)ccons - 1u - jn) & 63u)) & 1);
-    const uint64_t corr = __builtin_amdgcn_ballot_w64(cb);
-    uint64_t newm = __builtin_amdgcn_ballot_w64(in_z && ((rmask >> (jz & 63u)) & 1));
-    uint64_t negm = __builtin_amdgcn_ballot_w64(in_z && ((rmask >> (jz & 63u)) & 1) && !((smask >> (jz & 63u)) & 1));
+    const uint64_t corr = __builtin_amdgcn_ballot_w64(in_n && (cb & 1u));
+    uint64_t newm = __builtin_amdgcn_ballot_w64(in_z && (rb & 1u));
+    uint64_t negm = __builtin_amdgcn_ballot_w64(in_z && (rb & 1u) && !(rb & 2u));
     if (ovf >= 0) {
       newm |= 1ull << ovf;
       negm = ovf_pos ? (negm & ~(1ull << ovf)) : (negm | (1ull << ovf));
