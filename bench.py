@@ -357,18 +357,27 @@ def main():
             k[0] += 1
 
         # a fresh function's first steps allocate its pinned slots and start
-        # its copy pool: at least 50 untimed steps before the first timed leg
-        for _ in range(max(warm, 50) if fresh else 2 * args.host_depth):
+        # its copy pool: at least 50 untimed steps and 0.25 s before the first
+        # timed leg (a first leg right after the resident one ran up to 2x slower
+        # after 50 steps alone: profiles/r4/spin_ab_r4.txt)
+        t_w = time.perf_counter()
+        nw = 0
+        while nw < (max(warm, 50) if fresh else 2 * args.host_depth) or \
+                (fresh and time.perf_counter() - t_w < 0.25):
             hstep()
+            nw += 1
+        torch.cuda.synchronize()
         barrier()
         fn.pipeline.host_times(reset=True)
-        t = timed(hstep, args.steps, 0)
+        # each host leg times at least 100 steps (K = 20 batches of c2 are ~9 ms)
+        host_steps = max(args.steps, 100)
+        t = timed(hstep, host_steps, 0)
         fn.check()
         us, calls = fn.pipeline.host_times(reset=True)
         info = fn.pipeline.ctxs[0].host_info()
         if register:
             fn.release()
-        return B * args.steps * world / t, {k_: round(v / max(calls, 1), 1) for k_, v in us.items()}, info, fn
+        return B * host_steps * world / t, {k_: round(v / max(calls, 1), 1) for k_, v in us.items()}, info, fn
 
     if args.only_resident:
         args.dataset_batches = 0
@@ -490,8 +499,9 @@ def main():
     if value_host is not None:
         res["value_host_input"] = round(value_host, 1)
         res["value_host_input_per_gpu"] = round(value_host / world, 1)
-        res["value_host_input_note"] = ("the same steps with the cells in host pa.RecordBatches through the "
-                                        "pipelined to_tensor_fn (make_to_tensor_fn(depth)): pinned copy "
+        res["value_host_input_note"] = ("the same workload (max(steps, 100) timed steps per leg, after >= 50 "
+                                        "steps and 0.25 s of warm-up) with the cells in host pa.RecordBatches "
+                                        "through the pipelined to_tensor_fn (make_to_tensor_fn(depth)): pinned copy "
                                         "overlapped with the header walk, one H2D DMA per step on the "
                                         "device's copy stream; median of value_host_input_reps; "
                                         "value_host_registered: the same with the two batches' image buffers "
