@@ -15,6 +15,8 @@
 
 using namespace ldt;
 
+static bool g_print_scans = false; // PLAN_SCANS=1: also print each scan's (offset, length)
+
 static int plan_one(const uint8_t *cell, int64_t len) {
   Header H;
   int st = walk_markers(cell, len, H);
@@ -24,6 +26,8 @@ static int plan_one(const uint8_t *cell, int64_t len) {
     ProgPlan P;
     st = plan_progressive(cell, len, H, P);
     if (st != LDT_IMG_OK) return st;
+    if (g_print_scans)
+      for (const auto &sc : P.scans) printf("%lld:%lld ", (long long)sc.data_off, (long long)sc.data_len);
     for (const auto &t : P.tabs) {
       ProgTab pt;
       if (!build_prog_tab(t.first, t.second, pt)) return LDT_IMG_NOT_JPEG;
@@ -40,6 +44,7 @@ static int plan_one(const uint8_t *cell, int64_t len) {
 }
 
 int main() {
+  g_print_scans = getenv("PLAN_SCANS") != nullptr;
   uint32_t n;
   while (fread(&n, 4, 1, stdin) == 1) {
     uint8_t *cell = (uint8_t *)malloc(n ? n : 1);

@@ -49,6 +49,7 @@ def planner(tmp_path_factory):
         out = [int(x) for x in r.stdout.split()]
         assert len(out) == len(cells)
         return out
+    run.exe = exe
     return run
 
 
@@ -187,3 +188,76 @@ def test_progressive_scan_header_overwrites(planner):
                 cells.append(bytes(x))
     got = planner(cells)
     assert all(0 <= s <= 5 for s in got)
+
+
+def test_progressive_scan_ranges(planner):
+    """plan_progressive's scan byte ranges (the SSE2 end-of-scan search) against
+    a byte-by-byte restatement: the first 0xFF followed by a byte that is not
+    0x00, 0xFF or RSTn ends a scan. Progressive goldens, synthetic images with
+    restart intervals, and copies whose scans were salted with 0xFF 0x00 /
+    0xFF 0xFF / 0xFF RSTn pairs at random offsets (16-byte-boundary cases
+    included)."""
+    import subprocess as sp
+
+    from ldt_amd import synth
+
+    def ref_ranges(b):
+        out, i = [], 2
+        while i + 4 <= len(b):
+            if b[i] != 0xFF:
+                return None
+            while i + 1 < len(b) and b[i + 1] == 0xFF:
+                i += 1
+            m = b[i + 1]
+            if m == 0xD9:
+                break
+            if m == 0x01 or 0xD0 <= m <= 0xD7:
+                i += 2
+                continue
+            n = (b[i + 2] << 8) | b[i + 3]
+            if m != 0xDA:
+                i += 2 + n
+                continue
+            s0 = i + 2 + n
+            j = s0
+            while j + 1 < len(b) and not (b[j] == 0xFF and b[j + 1] not in (0x00, 0xFF) and not 0xD0 <= b[j + 1] <= 0xD7):
+                j += 1
+            out.append((s0, j - s0))
+            i = j
+        return out
+
+    cells = [open(e, "rb").read() for e in sorted(glob.glob(os.path.join(GOLDEN, "jpeg", "*.jpg")))
+             if "prog" in os.path.basename(e)]
+    assert len(cells) >= 5
+    cells += [synth.encode(synth.field(96 + 17 * k, 80 + 9 * k, k, 12.0), quality=90, progressive=True,
+                           **({"restart_marker_blocks": 2} if k % 2 else {})) for k in range(6)]
+    rng = np.random.default_rng(7)
+    salted = []
+    for b in cells[:6]:
+        rr = ref_ranges(b)
+        bb = bytearray(b)
+        for (s0, ln) in rr:
+            for _ in range(6):
+                if ln < 40:
+                    break
+                p = s0 + int(rng.integers(2, ln - 4))
+                if bb[p - 1] == 0xFF:
+                    continue
+                bb[p:p + 2] = bytes([0xFF, int(rng.choice([0x00, 0xFF, 0xD3]))])
+        salted.append(bytes(bb))
+    cells += salted
+    inp = b"".join(struct.pack("<I", len(c)) + c for c in cells)
+    r = sp.run([planner.exe], input=inp, capture_output=True, timeout=300,
+               env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0", PLAN_SCANS="1"))
+    assert r.returncode == 0 and not r.stderr, r.stderr.decode(errors="replace")[-2000:]
+    lines = r.stdout.decode().splitlines()
+    assert len(lines) == len(cells)
+    checked = 0
+    for b, line in zip(cells, lines):
+        parts = line.split()
+        if parts[-1] != "0":
+            continue
+        got = [tuple(int(x) for x in t.split(":")) for t in parts[:-1]]
+        assert got == ref_ranges(b), (got[:3], ref_ranges(b)[:3])
+        checked += 1
+    assert checked >= len(cells) - len(salted)
