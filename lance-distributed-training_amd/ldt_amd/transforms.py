@@ -546,6 +546,27 @@ class ResidentBatch:
         return out, out_lbl
 
 
+def slot_streams(depth: int, queues: int, env: Optional[str] = None) -> Tuple[int, bool]:
+    """DecodePipeline's stream plan for ``depth`` slots on a process with
+    ``queues`` HIP hardware queues per priority (GPU_MAX_HW_QUEUES): returns
+    (slots on high-priority streams, cells' DMA on the slots' own streams).
+
+    Normal priority while the slots and the consumer's stream fit the queues;
+    deeper pipelines put up to ``queues`` slots on high-priority streams (their
+    own queues) and the rest beside the consumer. The copy stream needs a
+    normal queue of its own beside normal slots, and beside high-priority slots
+    it measured slower when normal slots share the pool too (c2p depth 6: host
+    input 35k vs 50k at depth 7 with the DMA on the slots' streams).
+    ``env`` (LDT_SLOT_PRIORITY) "0"/"1" forces every slot's priority."""
+    if env is not None:
+        n_high = depth if int(env) else 0
+    else:
+        n_high = 0 if depth + 1 <= queues else min(depth, queues)
+    n_normal = depth - n_high
+    slot_dma = (n_normal + 2 > queues or n_high > 0) if n_normal else (n_high > queues)
+    return n_high, slot_dma
+
+
 class DecodePipeline:
     """`depth` batches in flight: each slot owns a libldt context (its own HBM
     workspace and pinned staging ring) and a HIP stream. ``decode(batch)``
@@ -585,18 +606,9 @@ class DecodePipeline:
         # consumer's stream (a shared queue serialises the slots: measured
         # c2p depth 4: 26k img/s on normal streams vs 44k). LDT_SLOT_PRIORITY
         # = 0 / 1 forces either.
-        q = _lib.hw_queues()
-        env = os.environ.get("LDT_SLOT_PRIORITY")
-        if env is not None:
-            n_high = self.depth if int(env) else 0
-        else:  # up to q high-priority slots, the rest beside the consumer's stream
-            n_high = 0 if self.depth + 1 <= q else min(self.depth, q)
-        n_normal = self.depth - n_high
+        n_high, slot_dma = slot_streams(self.depth, _lib.hw_queues(), os.environ.get("LDT_SLOT_PRIORITY"))
         self.high_priority = n_high > 0
-        # the cells' DMA on the copy stream needs a normal queue of its own, and
-        # beside a mixed set of slots it measured slower (c2p depth 6: host
-        # input 35k vs 50k at depth 7 with the DMA on the slots' streams)
-        if (n_normal + 2 > q or n_high > 0) if n_normal else (n_high > q):
+        if slot_dma:
             for c in self.ctxs:
                 c.set_option(_lib.OPT_COPY_MODE, 1)
         self.streams = [torch.cuda.Stream(self.dec.device, priority=-1 if i < n_high else 0)

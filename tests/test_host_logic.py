@@ -164,3 +164,21 @@ def test_fused_destuff_classification_matches_per_byte_rules(tmp_path):
     r = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout
+
+
+def test_slot_stream_plan():
+    """DecodePipeline's stream plan (transforms.slot_streams): normal streams
+    while the slots + the consumer's stream fit the hardware queues, high
+    priority for deeper pipelines (up to one pool of queues), the cells' DMA on
+    the slots' streams whenever the copy stream would share a queue."""
+    from ldt_amd.transforms import slot_streams
+
+    assert slot_streams(2, 4) == (0, False)   # c2 host legs: copy stream
+    assert slot_streams(3, 4) == (0, True)    # c2 resident: 3 slots + consumer + copy > 4
+    assert slot_streams(4, 4) == (4, False)   # all high priority, copy stream beside the consumer
+    assert slot_streams(7, 4) == (4, True)    # 4 high + 3 normal: DMA on the slots
+    assert slot_streams(8, 4) == (4, True)
+    assert slot_streams(6, 8) == (0, False)   # 6 slots + consumer + copy stream fit 8 queues
+    assert slot_streams(7, 8) == (0, True)
+    assert slot_streams(3, 4, "1") == (3, False)
+    assert slot_streams(7, 4, "0") == (0, True)
