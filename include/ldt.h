@@ -66,14 +66,19 @@ extern "C" {
                                  S >= this that fits its slots in 1024 lanes   */
 #define LDT_OPT_PROFILE 4     /* 1: record HIP events around every stage on the
                                  caller's stream (read with ldt_stage_times)    */
-#define LDT_OPT_RESIZE_IMPL 5 /* 0 auto (default) and 1: one wave per band
+#define LDT_OPT_RESIZE_IMPL 5 /* 0 auto (default): one wave per band
                                  (k_resize4), the streaming workgroup kernel for
-                                 sources wider than 1120 px; 2: the streaming
-                                 kernel for all (cross-check); 3: 4:2:0 sources
-                                 <= 512 px wide two waves per band
+                                 sources wider than 1120 px, 4:2:0 sources
+                                 <= 512 px wide with the fancy upsampling on
+                                 packed 16-bit pairs (k_resize4<5>); 1: the
+                                 same with 32-bit upsampling (k_resize4<0>,
+                                 round 3's default, cross-check); 2: the
+                                 streaming kernel for all (cross-check); 3: 4:2:0
+                                 sources <= 512 px wide two waves per band
                                  (k_resize420, cross-check; slower); 4: the
                                  same sources one staged row per step, 4 waves
-                                 per SIMD (k_resize4r, cross-check; no faster) */
+                                 per SIMD (k_resize4r, cross-check; no faster);
+                                 5: the packed 16-bit staging (as 0) */
 #define LDT_OPT_SYNC_WARM 7   /* parallel decoder phase 1 starts this % of S
                                  before each range (0..200, default 0)         */
 #define LDT_OPT_COPY_THREADS 8 /* threads of the context's host copy pool that

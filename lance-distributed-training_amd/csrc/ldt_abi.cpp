@@ -955,7 +955,9 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   }
   p.warm_pct = c->warm_pct;
   p.resize_waves_pct = c->resize_waves_pct;
-  p.resize420 = c->resize_impl == 3 ? 1 : (c->resize_impl == 4 ? 2 : 0);
+  // 4:2:0 sources <= 512 px: 0 / 5 the packed 16-bit staging (k_resize4<5>),
+  // 1 the 32-bit staging (k_resize4<0>), 3 k_resize420, 4 k_resize4r
+  p.resize420 = c->resize_impl == 3 ? 1 : (c->resize_impl == 4 ? 2 : (c->resize_impl == 1 ? 0 : 3));
   p.n_chunks = n_chunks;
   p.n_ds_img = n_ds_img;
   p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
@@ -1170,7 +1172,7 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     c->warm_pct = (int)value;
     return LDT_OK;
   case LDT_OPT_RESIZE_IMPL:
-    if (value < 0 || value > 4) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
+    if (value < 0 || value > 5) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
     c->resize_impl = (int)value;
     return LDT_OK;
   case LDT_OPT_SUBSEQ_BITS:

@@ -142,6 +142,67 @@ __device__ __forceinline__ void bytes6(uint32_t w, int lane, int rc, int s[6]) {
   for (int i = 2; i <= 5; ++i) s[i] = i > rc ? e : s[i];
 }
 
+// ---- packed 16-bit fancy upsampling (SRC 5) ----
+// A chroma row dword w holds the lane's 4 samples (columns 4*lane..+3); the
+// upsampling context s[0..5] is columns 4*lane-1 .. 4*lane+4, with bytes6's
+// edge rules (column -1 -> column 0, columns past the last one -> the last).
+// Pairs (s[i], s[i+1]) are built as u16x2 by v_perm_b32 from the previous
+// lane's dword, w and the next lane's dword, with per-lane byte selectors
+// that encode the edge rules once (0x0C selects a zero byte).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+struct Pk5 {
+  u16x2 x01, x12, x23, x34, x45;
+};
+
+__device__ __forceinline__ void pk_selectors(int lane, int rc, uint32_t sel[5]) {
+  int src[6];
+  src[0] = lane == 0 ? 0 : 7; // previous lane's byte 3 (S0 = prev)
+#pragma unroll
+  for (int i = 1; i <= 4; ++i) src[i] = min(i, rc) - 1;
+  src[5] = rc == 5 ? 4 : rc - 1; // next lane's byte 0 (S0 = next)
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+    sel[i] = (uint32_t)src[i] | (0x0Cu << 8) | ((uint32_t)src[i + 1] << 16) | (0x0Cu << 24);
+}
+
+__device__ __forceinline__ u16x2 as_pk(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+
+__device__ __forceinline__ Pk5 pairs5(uint32_t w, const uint32_t sel[5]) {
+  const uint32_t p = from_prev_lane(w), n = from_next_lane(w);
+  Pk5 r;
+  r.x01 = as_pk(__builtin_amdgcn_perm(p, w, sel[0]));
+  r.x12 = as_pk(__builtin_amdgcn_perm(n, w, sel[1]));
+  r.x23 = as_pk(__builtin_amdgcn_perm(n, w, sel[2]));
+  r.x34 = as_pk(__builtin_amdgcn_perm(n, w, sel[3]));
+  r.x45 = as_pk(__builtin_amdgcn_perm(n, w, sel[4]));
+  return r;
+}
+
+// One output row of h2v2_fancy_upsample from the nearer chroma row A and the
+// farther one F: T = 3A + F (vertical), then out[j] = (3T[ci] + T[ci -+ 1] +
+// 8 - (j & 1)) >> 4, ci = j/2 + 1. ev[m] = (out[4m], out[4m+2]),
+// od[m] = (out[4m+1], out[4m+3]). Every value stays below 2^12.
+__device__ __forceinline__ void fancy_pk(const Pk5 &A, const Pk5 &F, u16x2 ev[2], u16x2 od[2]) {
+  const u16x2 three = {3, 3};
+  const u16x2 T01 = A.x01 * three + F.x01, T12 = A.x12 * three + F.x12, T23 = A.x23 * three + F.x23,
+              T34 = A.x34 * three + F.x34, T45 = A.x45 * three + F.x45;
+  const u16x2 c8 = {8, 8}, c7 = {7, 7};
+  ev[0] = (T12 * three + T01 + c8) >> 4;
+  ev[1] = (T34 * three + T23 + c8) >> 4;
+  od[0] = (T12 * three + T23 + c7) >> 4;
+  od[1] = (T34 * three + T45 + c7) >> 4;
+}
+
+// ycc_px with the -128 offsets folded into the rounding constants (the same
+// integers: 91881 (cr - 128) + 32768 = 91881 cr + (32768 - 91881 * 128)).
+__device__ __forceinline__ uint32_t ycc_px_raw(int y, int cb, int cr) {
+  const int r = y + ((__mul24(91881, cr) + (32768 - 91881 * 128)) >> 16);
+  const int g = y + ((__mul24(-22554, cb) + __mul24(-46802, cr) + (32768 + (22554 + 46802) * 128)) >> 16);
+  const int b = y + ((__mul24(116130, cb) + (32768 - 116130 * 128)) >> 16);
+  return rgbx(clampi(r, 0, 255), clampi(g, 0, 255), clampi(b, 0, 255));
+}
+
 } // namespace
 
 struct Geom4 {
@@ -182,7 +243,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   // Skewed staging for raw rows (c5: 4-5-way tap conflicts otherwise, and the
   // kernel is LDS-bound). JPEG rows stay plain: the skew's extra registers
   // cost a wave per SIMD there, which is worth more than its 2-way conflicts.
-  constexpr bool kJpeg = SRC == 0 || SRC == 2 || SRC == 4;
+  constexpr bool kJpeg = SRC == 0 || SRC == 2 || SRC == 4 || SRC == 5;
   constexpr bool kRow = SRC == 4; // one staged row per step
   constexpr bool kSkew = !kJpeg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -204,7 +265,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
       for (int i = lane; i < per; i += 64) o[c * (kOut * kOut / 4) + i] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
-  if (kJpeg && resize_fast420(descs[img]) != (SRC == 0 || SRC == 4)) return;
+  if (kJpeg && resize_fast420(descs[img]) != (SRC == 0 || SRC == 4 || SRC == 5)) return;
   int W, H;
   if constexpr (kJpeg) {
     W = descs[img].width;
@@ -267,7 +328,8 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   }
 
   // JPEG fast path: 4:2:0 with both chroma planes fancy-upsampled, W <= 512
-  constexpr bool fast420 = SRC == 0 || SRC == 4;
+  constexpr bool fast420 = SRC == 0 || SRC == 4 || SRC == 5;
+  constexpr bool kPk = SRC == 5; // packed 16-bit fancy upsampling
   int rc = 5, cdh = 1;
   // plane geometry copied to registers once: the wave fences in process()
   // would otherwise make every fetch reload it (a dependent global round trip
@@ -276,6 +338,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   int ps0 = 0, ps1 = 0;
   const ImgDesc *dp = nullptr;
   const uint8_t *raw_cell = nullptr;
+  uint32_t psel[5] = {0u, 0u, 0u, 0u, 0u};
   constexpr bool raw_al16 = SRC == 1;
   if constexpr (kJpeg) {
     dp = descs + img;
@@ -283,6 +346,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
     const int dw = d.cdw[1];
     rc = lane == (dw - 1) / 4 ? (dw - 1) % 4 + 1 : 5;
     cdh = d.cdh[1];
+    if constexpr (kPk) pk_selectors(lane, rc, psel);
     po0 = d.plane_off[0];
     po1 = d.plane_off[1];
     po2 = d.plane_off[2];
@@ -378,7 +442,40 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
       (void)s1;
     } else if constexpr (kJpeg) {
       const ImgDesc &d = *dp;
-      if constexpr (fast420) {
+      if constexpr (kPk) {
+        // the same h2v2 fancy upsampling on packed 16-bit pairs: both output
+        // rows' 8 chroma samples of a component in 4 packed registers each
+        const int x0 = lane * 8;
+        u16x2 ev[2][2][2], od[2][2][2]; // [comp][row][pair]
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const Pk5 A = pairs5(jp.c[c][1], psel), U = pairs5(jp.c[c][0], psel),
+                    D = pairs5(jp.c[c][2], psel);
+          fancy_pk(A, U, ev[c][0], od[c][0]);
+          fancy_pk(A, D, ev[c][1], od[c][1]);
+        }
+        uint32_t p0[8], p1[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t ya_ = j < 4 ? jp.y0.x : jp.y0.y, yb_ = j < 4 ? jp.y1.x : jp.y1.y;
+          const int sh = 8 * (j & 3);
+          // sample j: even j from ev, odd from od; pair j >> 2, half (j >> 1) & 1
+          const int pr = j >> 2, hf = (j >> 1) & 1;
+          const u16x2 cb0 = (j & 1) ? od[0][0][pr] : ev[0][0][pr], cr0 = (j & 1) ? od[1][0][pr] : ev[1][0][pr];
+          const u16x2 cb1 = (j & 1) ? od[0][1][pr] : ev[0][1][pr], cr1 = (j & 1) ? od[1][1][pr] : ev[1][1][pr];
+          p0[j] = ycc_px_raw((int)((ya_ >> sh) & 255), hf ? cb0.y : cb0.x, hf ? cr0.y : cr0.x);
+          p1[j] = ycc_px_raw((int)((yb_ >> sh) & 255), hf ? cb1.y : cb1.x, hf ? cr1.y : cr1.x);
+        }
+        if (x0 < W) {
+          uint4 *d0 = reinterpret_cast<uint4 *>(s0 + x0);
+          uint4 *d1 = reinterpret_cast<uint4 *>(s1 + x0);
+          d0[0] = make_uint4(p0[0], p0[1], p0[2], p0[3]);
+          d0[1] = make_uint4(p0[4], p0[5], p0[6], p0[7]);
+          d1[0] = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+          d1[1] = make_uint4(p1[4], p1[5], p1[6], p1[7]);
+        }
+        (void)d;
+      } else if constexpr (fast420) {
         const int x0 = lane * 8;
         int cb[2][8], crr[2][8];
 #pragma unroll
@@ -1002,6 +1099,9 @@ bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t
       case 5: *err = launch_w2<5>(p, w, out, out_labels, g2, s); break;
       default: *err = launch_w2<7>(p, w, out, out_labels, g2, s); break;
       }
+    } else if (p.resize420 == 3) {
+      if (!dispatch4<5>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s, err))
+        return false;
     } else if (!dispatch4<0>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s,
                              err)) {
       return false;

@@ -374,9 +374,11 @@ def test_tall_bands_large_batches():
 
 
 def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
-    """The default resize (k_resize4, one wave per band), the banded
+    """The default resize (k_resize4, one wave per band, packed 16-bit 4:2:0
+    staging), its 32-bit staging (LDT_OPT_RESIZE_IMPL=1), the banded
     workgroup kernel (LDT_OPT_RESIZE_IMPL=2), the two-waves-per-band 4:2:0
-    kernel (=3) and the single-row 4:2:0 kernel (=4, k_resize4r) give
+    kernel (=3), the single-row 4:2:0 kernel (=4, k_resize4r) and the packed
+    16-bit 4:2:0 staging (=5, k_resize4<5>) give
     identical tensors on every golden image, on a
     c2/c1-shaped batch and on unaligned raw cells; a batch with a truncated
     image leaves nothing behind that changes the next batch."""
@@ -395,7 +397,7 @@ def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
     mixed = synth.q90_512(6, seed=8)[0] + synth.food101_like(10, seed=9)[0]
     res = {}
     try:
-        for impl in (0, 2, 3, 4):
+        for impl in (0, 1, 2, 3, 4, 5):
             ctx.set_option(_lib.OPT_RESIZE_IMPL, impl)
             a = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
             b = ldt_amd.resize_raw(arr, 301, 517, normalize=True).cpu().numpy()
@@ -403,7 +405,7 @@ def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
             res[impl] = (a, b, c)
     finally:
         ctx.set_option(_lib.OPT_RESIZE_IMPL, 0)
-    for impl in (2, 3, 4):
+    for impl in (1, 2, 3, 4, 5):
         for k in range(3):
             assert np.array_equal(res[0][k], res[impl][k]), (impl, k)
     for k in (0, 5, 6, 15):
