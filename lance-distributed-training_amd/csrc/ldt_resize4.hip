@@ -194,14 +194,23 @@ __device__ __forceinline__ void fancy_pk(const Pk5 &A, const Pk5 &F, u16x2 ev[2]
   od[1] = (T34 * three + T45 + c7) >> 4;
 }
 
-// ycc_px with the -128 offsets folded into the rounding constants (the same
-// integers: 91881 (cr - 128) + 32768 = 91881 cr + (32768 - 91881 * 128)).
-__device__ __forceinline__ uint32_t ycc_px_raw(int y, int cb, int cr) {
-  const int r = y + ((__mul24(91881, cr) + (32768 - 91881 * 128)) >> 16);
-  const int g = y + ((__mul24(-22554, cb) + __mul24(-46802, cr) + (32768 + (22554 + 46802) * 128)) >> 16);
-  const int b = y + ((__mul24(116130, cb) + (32768 - 116130 * 128)) >> 16);
-  return rgbx(clampi(r, 0, 255), clampi(g, 0, 255), clampi(b, 0, 255));
+// jdcolor.c ycc_rgb_convert for the planar staging (SRC 5): each channel's
+// value before the >> 16, with Y << 16 and the -128 offsets folded in (the
+// same integers: y + ((91881 (cr - 128) + 32768) >> 16) = (Y16 + 91881 cr +
+// 32768 - 91881 * 128) >> 16, an arithmetic shift), clamped to [0, 2^24):
+// byte 2 is the clamped channel value. Luma byte `jb` of the dword yw.
+__device__ __forceinline__ void ycc_x(uint32_t yw, int jb, int cb, int cr, uint32_t &xr, uint32_t &xg,
+                                      uint32_t &xb) {
+  // Y << 16: luma byte jb moved to byte 2 (0x0C selects zero bytes)
+  const int y16 = (int)__builtin_amdgcn_perm(0u, yw, 0x0C000C0Cu | ((uint32_t)jb << 16));
+  const int r = __mul24(91881, cr) + (y16 + (32768 - 91881 * 128));
+  const int g = __mul24(-22554, cb) + __mul24(-46802, cr) + (y16 + (32768 + (22554 + 46802) * 128));
+  const int b = __mul24(116130, cb) + (y16 + (32768 - 116130 * 128));
+  xr = (uint32_t)min(max(r, 0), 0xFFFFFF);
+  xg = (uint32_t)min(max(g, 0), 0xFFFFFF);
+  xb = (uint32_t)min(max(b, 0), 0xFFFFFF);
 }
+
 
 } // namespace
 
@@ -454,25 +463,25 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
           fancy_pk(A, U, ev[c][0], od[c][0]);
           fancy_pk(A, D, ev[c][1], od[c][1]);
         }
-        uint32_t p0[8], p1[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t ya_ = j < 4 ? jp.y0.x : jp.y0.y, yb_ = j < 4 ? jp.y1.x : jp.y1.y;
-          const int sh = 8 * (j & 3);
-          // sample j: even j from ev, odd from od; pair j >> 2, half (j >> 1) & 1
-          const int pr = j >> 2, hf = (j >> 1) & 1;
-          const u16x2 cb0 = (j & 1) ? od[0][0][pr] : ev[0][0][pr], cr0 = (j & 1) ? od[1][0][pr] : ev[1][0][pr];
-          const u16x2 cb1 = (j & 1) ? od[0][1][pr] : ev[0][1][pr], cr1 = (j & 1) ? od[1][1][pr] : ev[1][1][pr];
-          p0[j] = ycc_px_raw((int)((ya_ >> sh) & 255), hf ? cb0.y : cb0.x, hf ? cr0.y : cr0.x);
-          p1[j] = ycc_px_raw((int)((yb_ >> sh) & 255), hf ? cb1.y : cb1.x, hf ? cr1.y : cr1.x);
-        }
-        if (x0 < W) {
-          uint4 *d0 = reinterpret_cast<uint4 *>(s0 + x0);
-          uint4 *d1 = reinterpret_cast<uint4 *>(s1 + x0);
-          d0[0] = make_uint4(p0[0], p0[1], p0[2], p0[3]);
-          d0[1] = make_uint4(p0[4], p0[5], p0[6], p0[7]);
-          d1[0] = make_uint4(p1[0], p1[1], p1[2], p1[3]);
-          d1[1] = make_uint4(p1[4], p1[5], p1[6], p1[7]);
+        for (int r = 0; r < 2; ++r) {
+          uint32_t px[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t yw = r ? (j < 4 ? jp.y1.x : jp.y1.y) : (j < 4 ? jp.y0.x : jp.y0.y);
+            // sample j: even j from ev, odd from od; pair j >> 2, half (j >> 1) & 1
+            const int pr = j >> 2, hf = (j >> 1) & 1;
+            const u16x2 cb = (j & 1) ? od[0][r][pr] : ev[0][r][pr], cr = (j & 1) ? od[1][r][pr] : ev[1][r][pr];
+            uint32_t xr, xg, xb;
+            ycc_x(yw, j & 3, hf ? cb.y : cb.x, hf ? cr.y : cr.x, xr, xg, xb);
+            // RGBx: bytes 2 of xr, xg, xb
+            px[j] = __builtin_amdgcn_perm(xb, __builtin_amdgcn_perm(xg, xr, 0x0C0C0602u), 0x0C060100u);
+          }
+          if (x0 < W) {
+            uint4 *dq = reinterpret_cast<uint4 *>((r ? s1 : s0) + x0);
+            dq[0] = make_uint4(px[0], px[1], px[2], px[3]);
+            dq[1] = make_uint4(px[4], px[5], px[6], px[7]);
+          }
         }
         (void)d;
       } else if constexpr (fast420) {
