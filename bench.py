@@ -214,6 +214,8 @@ def main():
                     help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize4; 3 k_resize420 for 4:2:0)")
     ap.add_argument("--resize-waves-pct", type=int, default=0,
                     help="LDT_OPT_RESIZE_WAVES_PCT of every context (0: the library default, 100)")
+    ap.add_argument("--resize-wg-waves", type=int, default=0,
+                    help="LDT_OPT_RESIZE_WG_WAVES of every context (0: the library default, 2)")
     ap.add_argument("--no-config-legs", action="store_true",
                     help="skip the configs[2]/configs[3] dataset legs (c3, c4) of a c2 run")
     ap.add_argument("--no-registered", action="store_true",
@@ -327,6 +329,8 @@ def main():
         pipe.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
         if args.resize_waves_pct:
             pipe.set_option(_lib.OPT_RESIZE_WAVES_PCT, args.resize_waves_pct)
+        if args.resize_wg_waves:
+            pipe.set_option(_lib.OPT_RESIZE_WG_WAVES, args.resize_wg_waves)
 
         def step():
             b = batches[it[0] % nb]

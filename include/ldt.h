@@ -92,6 +92,11 @@ extern "C" {
                                  wave of resize waves on the device (10..1000,
                                  default 100); more bands fill the pipeline's
                                  CU gaps, fewer keep the kernel efficient      */
+#define LDT_OPT_RESIZE_WG_WAVES 15 /* waves (one band each) per k_resize4
+                                 workgroup for JPEG sources: 0 default (2),
+                                 1, 2 or 4; a 1-wave workgroup (~14 KB of LDS
+                                 at 512 px) fits beside a k_huff_image
+                                 workgroup of another batch on its CU      */
 #define LDT_OPT_FUSED_DESTUFF 11 /* 1 (default): the parallel Huffman decoder
                                  destuffs the scan bytes of an image whose
                                  stream fits its LDS window itself; 0: every

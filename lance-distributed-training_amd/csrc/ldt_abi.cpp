@@ -83,6 +83,7 @@ struct ldt_ctx {
   int warm_pct = 0;
   int subseq_bits = 256; // minimum S of the parallel decoder
   int resize_waves_pct = 100;
+  int resize_wpg = 0;
   bool fuse_destuff = LDT_FUSE_DEFAULT; // LDT_OPT_FUSED_DESTUFF
   int copy_threads = -1; // -1: default (from the cgroup quota per local rank, <= 6)
   bool copy_bind = true;  // LDT_OPT_COPY_BIND: pool threads on GPU-local cores
@@ -955,6 +956,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   }
   p.warm_pct = c->warm_pct;
   p.resize_waves_pct = c->resize_waves_pct;
+  p.resize_wpg = c->resize_wpg;
   // 4:2:0 sources <= 512 px: 0 / 5 the packed 16-bit staging (k_resize4<5>),
   // 1 the 32-bit staging (k_resize4<0>), 3 k_resize420, 4 k_resize4r
   p.resize420 = c->resize_impl == 3 ? 1 : (c->resize_impl == 4 ? 2 : (c->resize_impl == 1 ? 0 : 3));
@@ -1193,6 +1195,11 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
   case LDT_OPT_RESIZE_WAVES_PCT:
     if (value < 10 || value > 1000) return set_err(c, LDT_ERR_ARG, "resize waves %lld%%", (long long)value);
     c->resize_waves_pct = (int)value;
+    return LDT_OK;
+  case LDT_OPT_RESIZE_WG_WAVES:
+    if (value != 0 && value != 1 && value != 2 && value != 4)
+      return set_err(c, LDT_ERR_ARG, "resize waves per workgroup %lld", (long long)value);
+    c->resize_wpg = (int)value;
     return LDT_OK;
   case LDT_OPT_FUSED_DESTUFF:
     c->fuse_destuff = value != 0;

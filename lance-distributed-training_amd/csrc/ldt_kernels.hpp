@@ -36,6 +36,7 @@ struct DevPlan {
   int win_bytes;          // LDS window of k_huff_image (images needing more read global memory)
   int warm_pct;           // phase-1 warm-up before each range, % of S
   int resize_waves_pct;   // k_resize4 band count, % of one full wave of resize waves
+  int resize_wpg;         // k_resize4 waves per workgroup for JPEG sources (0: default 2)
   int resize420;          // 1: 4:2:0 images take k_resize420 (two waves per band); 2: k_resize4r (one staged row per step)
   int32_t *redo;          // debug counters of the parallel decoder (16 ints)
   int max_tabs;           // max distinct Huffman tables of one image (LDS slots)

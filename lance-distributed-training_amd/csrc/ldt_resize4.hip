@@ -222,6 +222,7 @@ struct Geom4 {
   int ntask;       // n * nbands
   int wave_bytes;  // LDS per wave
   int fill;        // JPEG: this launch zero-fills failed images' bands (label -100)
+  int wpg;         // waves (tasks) per workgroup
 };
 
 constexpr int kKvRows = 16; // vertical coefficient rows cached per wave
@@ -260,7 +261,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   for (int i = tid; i < 768; i += (int)blockDim.x) s_lut[i] = lut[i];
   __syncthreads(); // the only workgroup barrier
   // wave-uniform task: descriptor loads become scalar loads into SGPRs
-  const int task = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kResizeWaves + wave);
+  const int task = __builtin_amdgcn_readfirstlane((int)blockIdx.x * g.wpg + wave);
   if (task >= g.ntask) return;
   const int img = task / g.nbands, band = task - img * g.nbands;
   if (kJpeg && status[img] != 0) {
@@ -952,7 +953,9 @@ static int wave_bytes4(const Geom4 &g, int rows) {
 }
 
 // rows: staged source rows per step (2; 1 for the single-row 4:2:0 kernel)
-static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g, int rows = 2) {
+static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g, int rows = 2,
+                       int wpg = kResizeWaves) {
+  g.wpg = wpg;
   g.ks_v = resample_ksize_host(max_h, kOut);
   g.ring = g.ks_v + 1; // an output row is finished within 2 rows of its window end
   const int px = ((max_w + 15) / 16) * 16 + ks_h + 16;
@@ -964,7 +967,7 @@ static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, 
   g.bh = (kOut + nb - 1) / nb;
   g.nbands = (kOut + g.bh - 1) / g.bh;
   g.ntask = n * g.nbands;
-  return 3072 + kResizeWaves * (size_t)g.wave_bytes <= 160 * 1024;
+  return 3072 + g.wpg * (size_t)g.wave_bytes <= 160 * 1024;
 }
 
 template <int SRC, int KS>
@@ -974,9 +977,9 @@ static hipError_t launch4(const ImgDesc *descs, const uint8_t *planes, RawSrc ra
   static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resize4<SRC, KS>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  const int groups = (g.ntask + kResizeWaves - 1) / kResizeWaves;
-  hipLaunchKernelGGL((k_resize4<SRC, KS>), dim3(groups), dim3(64 * kResizeWaves),
-                     3072 + kResizeWaves * g.wave_bytes, s, descs,
+  const int groups = (g.ntask + g.wpg - 1) / g.wpg;
+  hipLaunchKernelGGL((k_resize4<SRC, KS>), dim3(groups), dim3(64 * g.wpg),
+                     3072 + g.wpg * g.wave_bytes, s, descs,
                      planes, raw, lut, labels, out, out_labels, status, g);
   return hipGetLastError();
 }
@@ -1010,7 +1013,8 @@ static hipError_t launch4r(const ImgDesc *descs, const uint8_t *planes, const fl
 // Waves to aim for: the CU count times the resident waves per CU the LDS
 // allows (at most 12; 16 for the single-row kernel, whose workgroups fit 8
 // per CU).
-static int waves_target4(const Geom4 &g, int pct, int max_wg = 6) {
+static int waves_target4(const Geom4 &g, int pct, int max_waves = 12) {
+  const int max_wg = max_waves / g.wpg;
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
@@ -1018,12 +1022,12 @@ static int waves_target4(const Geom4 &g, int pct, int max_wg = 6) {
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) cus = 256;
     else cus = prop.multiProcessorCount;
   }
-  int wg = (160 * 1024) / (3072 + kResizeWaves * g.wave_bytes);
+  int wg = (160 * 1024) / (3072 + g.wpg * g.wave_bytes);
   if (wg > max_wg) wg = max_wg;
   if (wg < 1) wg = 1;
   // LDT_OPT_RESIZE_WAVES_PCT: more, shorter bands fill the
   // pipeline's CU gaps better but cost the kernel's own efficiency
-  return cus * kResizeWaves * wg * (pct > 0 ? pct : 100) / 100;
+  return cus * g.wpg * wg * (pct > 0 ? pct : 100) / 100;
 }
 
 static int cu_count() {
@@ -1073,8 +1077,9 @@ bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t
   Geom4 g;
   const int ks_h = resample_ksize_host(p.max_w, kOut);
   if (ks_h > 11) return false;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g)) return false;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g)) return false;
+  const int wpg = p.resize_wpg > 0 ? p.resize_wpg : kResizeWaves;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, 2, wpg)) return false;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g, 2, wpg)) return false;
   RawSrc raw{nullptr, 0, 0, 0};
   // fast-path images and the rest go to separate kernels (each skips the
   // other's images); a batch of one kind launches one kernel. The first
@@ -1085,7 +1090,7 @@ bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t
     Geom4 gr;
     const int ks_f = resample_ksize_host(std::min(p.max_w, 512), kOut);
     if (ks_f <= 7 && make_geom4(p.n, std::min(p.max_w, 512), p.max_h, ks_f, 1, gr, 1) &&
-        make_geom4(p.n, std::min(p.max_w, 512), p.max_h, ks_f, waves_target4(gr, p.resize_waves_pct, 8), gr, 1)) {
+        make_geom4(p.n, std::min(p.max_w, 512), p.max_h, ks_f, waves_target4(gr, p.resize_waves_pct, 16), gr, 1)) {
       gr.fill = 1;
       switch (ks_f) {
       case 3: *err = launch4r<3>(p.descs, w.planes, p.lut, p.labels, out, out_labels, w.status, gr, s); break;

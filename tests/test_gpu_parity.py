@@ -403,8 +403,18 @@ def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
             b = ldt_amd.resize_raw(arr, 301, 517, normalize=True).cpu().numpy()
             c = ldt_amd.decode_tensor_image(_batch(mixed))["image"].cpu().numpy()
             res[impl] = (a, b, c)
+        for wpg in (1, 4):  # waves (bands) per k_resize4 workgroup
+            ctx.set_option(_lib.OPT_RESIZE_IMPL, 0)
+            ctx.set_option(_lib.OPT_RESIZE_WG_WAVES, wpg)
+            a = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+            c = ldt_amd.decode_tensor_image(_batch(mixed))["image"].cpu().numpy()
+            res[f"wpg{wpg}"] = (a, c)
     finally:
         ctx.set_option(_lib.OPT_RESIZE_IMPL, 0)
+        ctx.set_option(_lib.OPT_RESIZE_WG_WAVES, 0)
+    for wpg in (1, 4):
+        assert np.array_equal(res[0][0], res[f"wpg{wpg}"][0]), wpg
+        assert np.array_equal(res[0][2], res[f"wpg{wpg}"][1]), wpg
     for impl in (1, 2, 3, 4, 5):
         for k in range(3):
             assert np.array_equal(res[0][k], res[impl][k]), (impl, k)
