@@ -216,6 +216,8 @@ def main():
                     help="LDT_OPT_RESIZE_WAVES_PCT of every context (0: the library default, 100)")
     ap.add_argument("--resize-wg-waves", type=int, default=0,
                     help="LDT_OPT_RESIZE_WG_WAVES of every context (0: the library default, 2)")
+    ap.add_argument("--copy-bind", type=int, default=-1,
+                    help="LDT_OPT_COPY_BIND of the host legs (-1: the library default, 2)")
     ap.add_argument("--no-config-legs", action="store_true",
                     help="skip the configs[2]/configs[3] dataset legs (c3, c4) of a c2 run")
     ap.add_argument("--no-registered", action="store_true",
@@ -368,6 +370,8 @@ def main():
         if fresh:
             fn = ldt_amd.make_to_tensor_fn(depth=args.host_depth, device=dev, register=register)
             fn.pipeline.set_option(_lib.OPT_HOST_TIMING, 1)
+            if args.copy_bind >= 0:
+                fn.pipeline.set_option(_lib.OPT_COPY_BIND, args.copy_bind)
             fn.pipeline.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
         k = [0]
 

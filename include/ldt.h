@@ -107,10 +107,12 @@ extern "C" {
                                  `stream` waits for (the transfer overlaps the
                                  kernels of earlier batches); 1: the DMA on
                                  `stream` itself                              */
-#define LDT_OPT_COPY_BIND 13  /* 1 (default): copy-pool threads bound to
+#define LDT_OPT_COPY_BIND 13  /* 2 (default): copy-pool threads placed on
                                  physical cores local to the GPU's NUMA node,
                                  spread over its L3 domains, the block of
-                                 cores chosen by LOCAL_RANK; 0: unbound         */
+                                 cores chosen by LOCAL_RANK, each thread free
+                                 to run on any CPU of its core's L3 domain;
+                                 1: each thread pinned to its core; 0: unbound */
 #define LDT_OPT_COPY_NT 14    /* 1 (default): the copy pool writes the pinned slot with
                                  non-temporal stores (AVX2, default); 0: memcpy */
 

@@ -86,7 +86,7 @@ struct ldt_ctx {
   int resize_wpg = 0;
   bool fuse_destuff = LDT_FUSE_DEFAULT; // LDT_OPT_FUSED_DESTUFF
   int copy_threads = -1; // -1: default (from the cgroup quota per local rank, <= 6)
-  bool copy_bind = true;  // LDT_OPT_COPY_BIND: pool threads on GPU-local cores
+  int copy_bind = 2;      // LDT_OPT_COPY_BIND: pool threads on GPU-local cores' L3 domains (1: the cores)
   bool copy_nt = true;    // LDT_OPT_COPY_NT: non-temporal stores into the slot
   int copy_mode = 0;      // LDT_OPT_COPY_MODE: 0 DMA on the device's copy stream, 1 on the caller's
   bool host_timing = false;
@@ -262,8 +262,8 @@ CopyPool &copier(ldt_ctx *c) {
       (void)hipGetLastError();
       bus[0] = 0;
     }
-    c->placement = copy_placement(bus, c->copy_threads, c->copy_bind);
-    c->copier.reset(new CopyPool(c->placement.cpus, c->copy_nt));
+    c->placement = copy_placement(bus, c->copy_threads, c->copy_bind != 0);
+    c->copier.reset(new CopyPool(c->placement.cpus, c->copy_nt, c->copy_bind == 2));
   }
   return *c->copier;
 }
@@ -1209,8 +1209,9 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     c->copy_mode = (int)value;
     return LDT_OK;
   case LDT_OPT_COPY_BIND:
-    if ((value != 0) != c->copy_bind) {
-      c->copy_bind = value != 0;
+    if (value < 0 || value > 2) return set_err(c, LDT_ERR_ARG, "copy bind %lld", (long long)value);
+    if ((int)value != c->copy_bind) {
+      c->copy_bind = (int)value;
       c->copier.reset();
     }
     return LDT_OK;
@@ -1268,7 +1269,7 @@ int ldt_host_info(ldt_ctx *c, char *buf, size_t len) {
                          "\"local_rank\": %d, \"local_world\": %d, \"l3_domains\": %d, \"candidate_cores\": %d, "
                          "\"copy_bind\": %d, \"copy_nt\": %d, \"copy_mode\": %d, \"local_cpulist\": \"%s\"}",
                          (int)P.cpus.size(), cpus.c_str(), P.gpu_numa, P.quota_cpus, P.local_rank, P.local_world,
-                         P.l3_domains, P.candidates, c->copy_bind ? 1 : 0, c->copy_nt ? 1 : 0, c->copy_mode,
+                         P.l3_domains, P.candidates, c->copy_bind, c->copy_nt ? 1 : 0, c->copy_mode,
                          P.local_cpulist.c_str());
   return w >= 0 && (size_t)w < len ? LDT_OK : set_err(c, LDT_ERR_ARG, "host info: buffer of %zu bytes too small", len);
 }

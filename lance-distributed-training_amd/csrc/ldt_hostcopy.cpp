@@ -171,8 +171,8 @@ CopyPlacement copy_placement(const char *pci_bus_id, int nthreads, bool bind) {
   return P;
 }
 
-CopyPool::CopyPool(const std::vector<int> &cpus, bool nt) : nt_(nt) {
-  for (int cpu : cpus) th_.emplace_back([this, cpu] { run(cpu); });
+CopyPool::CopyPool(const std::vector<int> &cpus, bool nt, bool l3) : nt_(nt) {
+  for (int cpu : cpus) th_.emplace_back([this, cpu, l3] { run(cpu, l3); });
 }
 
 CopyPool::~CopyPool() {
@@ -248,11 +248,21 @@ void CopyPool::work(uint32_t g, bool pool_thread) {
   }
 }
 
-void CopyPool::run(int cpu) {
+void CopyPool::run(int cpu, bool l3) {
   if (cpu >= 0) {
     cpu_set_t cs;
     CPU_ZERO(&cs);
     CPU_SET(cpu, &cs);
+    if (l3) {
+      // the core's L3 domain (SMT siblings included) within the affinity the
+      // thread inherited: a busy core does not hold the thread's wake-up
+      cpu_set_t inh;
+      CPU_ZERO(&inh);
+      if (pthread_getaffinity_np(pthread_self(), sizeof(inh), &inh) == 0)
+        for (int c : parse_cpulist(read_line("/sys/devices/system/cpu/cpu" + std::to_string(cpu) +
+                                             "/cache/index3/shared_cpu_list")))
+          if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &inh)) CPU_SET(c, &cs);
+    }
     (void)pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs); // best effort
   }
   uint64_t seen = 0;

@@ -52,7 +52,9 @@ CopyPlacement copy_placement(const char *pci_bus_id, int nthreads, bool bind);
 // one. nt: non-temporal AVX2 stores (when the CPU has AVX2).
 class CopyPool {
 public:
-  CopyPool(const std::vector<int> &cpus, bool nt);
+  // l3: each thread may run on any CPU of its core's L3 domain (inside the
+  // process affinity) instead of on that core alone
+  CopyPool(const std::vector<int> &cpus, bool nt, bool l3 = false);
   ~CopyPool();
   int threads() const { return (int)th_.size(); }
   void start(void *dst, const void *src, size_t n);
@@ -64,7 +66,7 @@ public:
 
 private:
   void work(uint32_t g, bool pool_thread);
-  void run(int cpu);
+  void run(int cpu, bool l3);
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_cv_;

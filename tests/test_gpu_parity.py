@@ -577,7 +577,7 @@ def test_copy_pool_sizes_and_host_times(threads):
         _check(ref[k], oracle.jpeg_to_tensor(cells[k]), f"copy threads {threads}")
 
 
-@pytest.mark.parametrize("mode,bind,nt", [(0, 1, 0), (1, 1, 0), (0, 0, 1)])
+@pytest.mark.parametrize("mode,bind,nt", [(0, 1, 0), (1, 1, 0), (0, 0, 1), (0, 2, 1)])
 def test_copy_modes_bit_exact(mode, bind, nt):
     """LDT_OPT_COPY_MODE / _BIND / _NT: host batches through a 2-deep pipeline,
     8 calls over alternating batches of different sizes, so each context's two
