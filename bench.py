@@ -218,6 +218,8 @@ def main():
                     help="LDT_OPT_RESIZE_WG_WAVES of every context (0: the library default, 2)")
     ap.add_argument("--copy-bind", type=int, default=-1,
                     help="LDT_OPT_COPY_BIND of the host legs (-1: the library default, 2)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="ID=VALUE: an extra ldt_set_option on every context of the resident leg (A/B runs)")
     ap.add_argument("--no-config-legs", action="store_true",
                     help="skip the configs[2]/configs[3] dataset legs (c3, c4) of a c2 run")
     ap.add_argument("--no-registered", action="store_true",
@@ -333,6 +335,9 @@ def main():
             pipe.set_option(_lib.OPT_RESIZE_WAVES_PCT, args.resize_waves_pct)
         if args.resize_wg_waves:
             pipe.set_option(_lib.OPT_RESIZE_WG_WAVES, args.resize_wg_waves)
+        for o in args.opt:
+            k, v = o.split("=")
+            pipe.set_option(int(k), int(v))
 
         def step():
             b = batches[it[0] % nb]
