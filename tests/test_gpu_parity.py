@@ -987,3 +987,30 @@ def test_status_tickets_hold_two_calls():
     st[:] = 0
     assert ctx.lib.ldt_fetch_status_ticket(ctx.handle, tickets[2], st.ctypes.data, 4) == _lib.LDT_ERR_IMAGE
     assert st.tolist() == [3, 0, 0, 0]
+
+
+def test_packed_420_staging_edge_widths():
+    """k_resize4<5> (the default 4:2:0 staging on packed 16-bit pairs) against
+    the 32-bit staging (LDT_OPT_RESIZE_IMPL=1) and the oracle on 4:2:0 images
+    whose chroma edge falls on every byte position of a lane's dword and on
+    lane 0 itself (widths 5-17: the first lane is also the last chroma lane),
+    on the 64-lane boundary (widths 127-129, 255-257) and up to the fast
+    path's 512-px limit (jdsample.c h2v2_fancy_upsample edge columns)."""
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    widths = [5, 6, 7, 8, 9, 10, 11, 12, 13, 15, 16, 17, 23, 31, 32, 33, 63, 64, 65, 100, 127, 128, 129,
+              255, 256, 257, 383, 497, 503, 504, 505, 509, 510, 511, 512]
+    cells = [synth.encode(synth.field(8 + (7 * i) % 41, w, 300 + i), quality=90) for i, w in enumerate(widths)]
+    ctx = _lib.get_context(0)
+    out = {}
+    try:
+        for impl in (1, 0):
+            ctx.set_option(_lib.OPT_RESIZE_IMPL, impl)
+            out[impl] = ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy()
+    finally:
+        ctx.set_option(_lib.OPT_RESIZE_IMPL, 0)
+    for k, w in enumerate(widths):
+        assert np.array_equal(out[0][k], out[1][k]), f"width {w}"
+    for k in (0, 4, 11, 22, 34):
+        _check(out[0][k], oracle.jpeg_to_tensor(cells[k]), f"w{widths[k]}")
