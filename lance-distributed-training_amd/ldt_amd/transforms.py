@@ -777,19 +777,56 @@ class DecodePipeline:
             raise ImageDecodeError(bad)
 
 
-def make_to_tensor_fn(depth: int = 2, device=None, normalize=None, prefetch: int = 0,
+# make_to_tensor_fn(depth=None): batches with fewer cell bytes than this run 3
+# deep (DMA on the slot streams), larger ones 2 deep beside the copy stream
+# (profiles/r4/host_depth_ab_r4hd.txt: 3.3 MB batches of 128 +10% at depth 3,
+# 17 MB batches of 256 steady only at depth 2)
+AUTO_DEPTH_SMALL_BYTES = 8 << 20
+
+
+def auto_host_depth(cell_bytes: int) -> int:
+    """Batches in flight that make_to_tensor_fn(depth=None) picks for a batch
+    of `cell_bytes` bytes of encoded cells."""
+    return 3 if 0 < cell_bytes < AUTO_DEPTH_SMALL_BYTES else 2
+
+
+def _cell_bytes(batch, col: str) -> int:
+    """Encoded bytes of a host RecordBatch's image cells (0 if unknown)."""
+    try:
+        if col not in batch.schema.names:
+            return 0
+        arr = _column(batch, col)
+        if isinstance(arr, pa.ChunkedArray):
+            arr = arr.combine_chunks()
+        off = arr.buffers()[1]
+        if pa.types.is_fixed_size_binary(arr.type):
+            return len(arr) * arr.type.byte_width
+        dt = np.int64 if pa.types.is_large_binary(arr.type) else np.int32
+        o = np.frombuffer(off, dtype=dt)
+        return int(o[arr.offset + len(arr)] - o[arr.offset])
+    except Exception:  # not a host binary column: keep the default
+        return 0
+
+
+def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, prefetch: int = 0,
                       register: bool = False, register_cap: int = 8, **fixed):
     """A pipelined ``to_tensor_fn`` for ``LanceDataset(..., to_tensor_fn=...)``
     (lance_iterable.py:53-59): each call enqueues its RecordBatch on one of
     `depth` contexts/streams and returns at once, so batch k+1's host copy and
-    kernels overlap batch k's. Depth 2 (the default) leaves the cells' copy
-    stream its own hardware queue (DecodePipeline): measured faster on host
-    batches than depth 3 with the DMA on the slot streams. The tensors are ready on torch's current stream
+    kernels overlap batch k's. Depth 2 leaves the cells' copy stream its own
+    hardware queue (DecodePipeline): measured faster on large host batches
+    than depth 3 with the DMA on the slot streams, which small batches prefer
+    (DESIGN.md §7a); the default (None) picks one of the two per function. The tensors are ready on torch's current stream
     (it waits for the slot's stream). Per-image errors are reported
     asynchronously: by ``fn.check()``, and at the latest when the slot is
     reused a second time (2 * `depth` calls later, when that batch finished
     long ago, so the check never stalls the host) — unlike the synchronous
     ``decode_tensor_image``.
+
+    ``depth=None``: chosen at the first call from its batch, 3 for batches of
+    fewer than 8 MB of encoded cells (FOOD101-shaped batches of 128), else 2
+    (``auto_host_depth``); options set through ``fn.pipeline`` before that
+    call carry over. The ``fn.iterate`` (prefetch) path keeps depth 2.
 
     ``prefetch=k`` (k < depth): ``LanceDataset`` iterates through
     ``fn.iterate`` instead, enqueueing the next k batches before yielding each
@@ -806,8 +843,20 @@ def make_to_tensor_fn(depth: int = 2, device=None, normalize=None, prefetch: int
     raising (ldt.h: such a range stays on the copying path)."""
     from collections import OrderedDict
 
-    pipe = DecodePipeline(depth=depth, device=device)
+    auto = depth is None
+    pipe = DecodePipeline(depth=2 if auto else depth, device=device)
     image_column = fixed.get("image_column", "image")
+    # depth=None: the options set on the first pipeline, replayed on the one
+    # the first batch picks
+    opts: list = []
+    if auto:
+        _set = pipe.set_option
+
+        def _recording_set_option(opt, value):
+            opts.append((opt, value))
+            _set(opt, value)
+
+        pipe.set_option = _recording_set_option
     owned: "OrderedDict[int, object]" = OrderedDict()  # registrations made here, LRU order
     reg_on = [bool(register)]
     # churn guard: unregistering synchronises the device, so a loader that hands
@@ -850,7 +899,16 @@ def make_to_tensor_fn(depth: int = 2, device=None, normalize=None, prefetch: int
             release()
 
     def to_tensor_fn(batch, **kwargs):
+        nonlocal pipe
         calls[0] += 1
+        if auto and calls[0] == 1:
+            d = auto_host_depth(_cell_bytes(batch, kwargs.get("image_column", image_column)))
+            if d != pipe.depth:
+                pipe = DecodePipeline(depth=d, device=device)
+                for opt, value in opts:
+                    pipe.set_option(opt, value)
+                to_tensor_fn.pipeline = pipe
+                to_tensor_fn.check = pipe.check
         maybe_register(batch, kwargs.get("image_column", image_column))
         pipe.check_slot(pipe.k % pipe.depth)
         img, lbl = pipe.decode(batch, normalize=kwargs.get("normalize", normalize),
@@ -868,7 +926,7 @@ def make_to_tensor_fn(depth: int = 2, device=None, normalize=None, prefetch: int
     to_tensor_fn.registering = lambda: reg_on[0]
     to_tensor_fn.pipeline = pipe
     to_tensor_fn.release = release
-    to_tensor_fn.prefetch = max(0, min(int(prefetch), depth - 1))
+    to_tensor_fn.prefetch = max(0, min(int(prefetch), pipe.depth - 1))
     def registered(batches):
         for b in batches:
             maybe_register(b, image_column)

@@ -1014,3 +1014,31 @@ def test_packed_420_staging_edge_widths():
         assert np.array_equal(out[0][k], out[1][k]), f"width {w}"
     for k in (0, 4, 11, 22, 34):
         _check(out[0][k], oracle.jpeg_to_tensor(cells[k]), f"w{widths[k]}")
+
+
+def test_make_to_tensor_fn_auto_depth():
+    """make_to_tensor_fn() (depth=None): a FOOD101-shaped first batch (< 8 MB
+    of cells) runs 3 deep, a c2-shaped one 2 deep; options set through
+    fn.pipeline before the first call carry over to the pipeline it picks;
+    every call bit-exact against the synchronous decode."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    small, ls = synth.food101_like(48, seed=61)
+    big, lb = synth.q90_512(130, seed=62)  # ~8.7 MB of cells
+    for cells, labels, want in ((small, ls, 3), (big, lb, 2)):
+        rb = _batch(cells, labels)
+        ref = ldt_amd.decode_tensor_image(rb)["image"].cpu().numpy()
+        fn = ldt_amd.make_to_tensor_fn()
+        fn.pipeline.set_option(_lib.OPT_COPY_BIND, 1)
+        fn.pipeline.set_option(_lib.OPT_COPY_THREADS, 2)
+        outs = [fn(rb) for _ in range(5)]
+        fn.check()
+        torch.cuda.synchronize()
+        assert fn.pipeline.depth == want
+        for o in outs:
+            assert np.array_equal(o["image"].cpu().numpy(), ref)
+        info = fn.pipeline.ctxs[0].host_info()
+        assert info["copy_bind"] == 1 and info["copy_threads"] == 2

@@ -182,3 +182,26 @@ def test_slot_stream_plan():
     assert slot_streams(7, 8) == (0, True)
     assert slot_streams(3, 4, "1") == (3, False)
     assert slot_streams(7, 4, "0") == (0, True)
+
+
+def test_auto_host_depth_from_cell_bytes():
+    """make_to_tensor_fn(depth=None) picks 3 in flight for batches under 8 MB
+    of encoded cells and 2 above (profiles/r4/host_depth_ab_r4hd.txt); the
+    cell bytes of a sliced binary / large_binary / fixed-size column are the
+    slice's value bytes, not its whole buffer's."""
+    from ldt_amd.transforms import AUTO_DEPTH_SMALL_BYTES, _cell_bytes, auto_host_depth
+
+    assert auto_host_depth(3_300_000) == 3          # FOOD101-shaped batch of 128
+    assert auto_host_depth(17_000_000) == 2         # c2 batch of 256
+    assert auto_host_depth(AUTO_DEPTH_SMALL_BYTES) == 2
+    assert auto_host_depth(0) == 2                  # unknown (not a host column)
+    cells = [bytes([k % 251]) * (100 + 7 * k) for k in range(40)]
+    for t in (pa.binary(), pa.large_binary()):
+        rb = pa.RecordBatch.from_arrays([pa.array(cells, t), pa.array(np.arange(40, dtype=np.int64))],
+                                        names=["image", "label"])
+        assert _cell_bytes(rb, "image") == sum(map(len, cells))
+        sl = rb.slice(5, 20)
+        assert _cell_bytes(sl, "image") == sum(map(len, cells[5:25]))
+    fx = pa.RecordBatch.from_arrays([pa.array([b"x" * 48] * 9, pa.binary(48))], names=["image"])
+    assert _cell_bytes(fx.slice(2, 5), "image") == 5 * 48
+    assert _cell_bytes(fx, "missing") == 0
