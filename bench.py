@@ -228,8 +228,9 @@ def main():
                     help="the resident leg alone (no host, dataset, config or standalone legs): the run a "
                          "rocprofv3 --stats summary of the line's timed launches is taken from")
     ap.add_argument("--host-depth", type=int, default=None,
-                    help="batches in flight of the host-input legs (make_to_tensor_fn(depth)): default 2 (with the "
-                         "cells' copy stream, depth + 2 streams fit the process's 4 hardware queues), 7 for "
+                    help="batches in flight of the host-input legs (make_to_tensor_fn(depth)): default "
+                         "make_to_tensor_fn's own choice (2 for batches of >= 8 MB of cells, with the cells' copy "
+                         "stream: depth + 2 streams fit the process's 4 hardware queues; 3 below), 7 for "
                          "progressive workloads (high-priority slot streams, DecodePipeline)")
     ap.add_argument("--host-reps", type=int, default=3,
                     help="back-to-back runs of the copying host-input leg (value_host_input = their median)")
@@ -243,7 +244,7 @@ def main():
     if args.depth is None:
         args.depth = 7 if progressive else 3
     if args.host_depth is None:
-        args.host_depth = 7 if progressive else 2
+        args.host_depth = 7 if progressive else 0  # 0: make_to_tensor_fn's own choice (depth=None)
 
     import numpy as np
     import torch
@@ -373,7 +374,7 @@ def main():
         reuse (a training loop keeps one), else a new one with a full warm-up."""
         fresh = fn is None
         if fresh:
-            fn = ldt_amd.make_to_tensor_fn(depth=args.host_depth, device=dev, register=register)
+            fn = ldt_amd.make_to_tensor_fn(depth=args.host_depth or None, device=dev, register=register)
             fn.pipeline.set_option(_lib.OPT_HOST_TIMING, 1)
             if args.copy_bind >= 0:
                 fn.pipeline.set_option(_lib.OPT_COPY_BIND, args.copy_bind)
@@ -390,7 +391,7 @@ def main():
         # after 50 steps alone: profiles/r4/spin_ab_r4.txt)
         t_w = time.perf_counter()
         nw = 0
-        while nw < (max(warm, 50) if fresh else 2 * args.host_depth) or \
+        while nw < (max(warm, 50) if fresh else 2 * fn.pipeline.depth) or \
                 (fresh and time.perf_counter() - t_w < 0.25):
             hstep()
             nw += 1
@@ -402,7 +403,7 @@ def main():
         t = timed(hstep, host_steps, 0)
         fn.check()
         us, calls = fn.pipeline.host_times(reset=True)
-        info = fn.pipeline.ctxs[0].host_info()
+        info = dict(fn.pipeline.ctxs[0].host_info(), host_depth=fn.pipeline.depth)
         if register:
             fn.release()
         return B * host_steps * world / t, {k_: round(v / max(calls, 1), 1) for k_, v in us.items()}, info, fn
@@ -537,7 +538,7 @@ def main():
                                         "page-locked in place (register=True), DMA without the host copy")
         res["host_us_per_call"] = host_us
         res["value_host_input_reps"] = [round(v, 1) for v in host_reps]
-        res["host_placement"] = dict(host_info, numa_bound_cpus=numa_cpus, host_depth=args.host_depth)
+        res["host_placement"] = dict(host_info, numa_bound_cpus=numa_cpus)
         res["host_ranks"] = host_ranks
     if value_registered is not None:
         res["value_host_registered"] = round(value_registered, 1)
