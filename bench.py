@@ -234,6 +234,8 @@ def main():
                          "progressive workloads (high-priority slot streams, DecodePipeline)")
     ap.add_argument("--host-reps", type=int, default=3,
                     help="back-to-back runs of the copying host-input leg (value_host_input = their median)")
+    ap.add_argument("--dataset-depth", type=int, default=None,
+                    help="batches in flight of the dataset legs (default: --depth; 0: make_to_tensor_fn's own choice)")
     ap.add_argument("--dataset-copy", action="store_true",
                     help="dataset legs through the copying to_tensor_fn instead of registering the mapped "
                          "fragments' image buffers")
@@ -243,6 +245,8 @@ def main():
     # high-priority streams, 3 beside the consumer's; profiles/r4/prog_ab_r4.txt)
     if args.depth is None:
         args.depth = 7 if progressive else 3
+    if args.dataset_depth is None:
+        args.dataset_depth = args.depth
     if args.host_depth is None:
         args.host_depth = 7 if progressive else 0  # 0: make_to_tensor_fn's own choice (depth=None)
 
@@ -644,7 +648,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     # 3 in flight as the resident leg: the configs' batches of 128 need the
     # concurrency more than the copy stream (DMA on the slot streams here,
     # DecodePipeline's choice at depth 3)
-    fn = ldt_amd.make_to_tensor_fn(depth=args.depth, device=dev, register=not args.dataset_copy)
+    fn = ldt_amd.make_to_tensor_fn(depth=args.dataset_depth or None, device=dev, register=not args.dataset_copy)
     fn.pipeline.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
     ds = ldt_amd.LanceDataset(path, batch_size=B, sampler=sampler, to_tensor_fn=fn)
 
@@ -679,7 +683,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
             "images_all_ranks": tot_imgs, "elapsed_ms_max": round(t * 1e3, 3),
             "timing": "full epochs per rank (plan + every batch, padding included) between barriers, "
                       "max over ranks",
-            "harness": (f"LanceDataset(path, batch_size, sampler, to_tensor_fn=make_to_tensor_fn(depth={args.depth}, "
+            "harness": (f"LanceDataset(path, batch_size, sampler, to_tensor_fn=make_to_tensor_fn(depth={fn.pipeline.depth}, "
                         f"register={not args.dataset_copy}))")}
     return tot_imgs / t, info
 

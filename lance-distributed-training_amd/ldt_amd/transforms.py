@@ -826,7 +826,9 @@ def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, 
     ``depth=None``: chosen at the first call from its batch, 3 for batches of
     fewer than 8 MB of encoded cells (FOOD101-shaped batches of 128), else 2
     (``auto_host_depth``); options set through ``fn.pipeline`` before that
-    call carry over. The ``fn.iterate`` (prefetch) path keeps depth 2.
+    call carry over. The ``fn.iterate`` (prefetch) path keeps depth 2. A
+    ``LanceDataset`` loop over registered (mapped) fragments should ask for
+    ``depth=3``.
 
     ``prefetch=k`` (k < depth): ``LanceDataset`` iterates through
     ``fn.iterate`` instead, enqueueing the next k batches before yielding each
@@ -844,6 +846,10 @@ def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, 
     from collections import OrderedDict
 
     auto = depth is None
+    # (registered sources have no size-independent best depth: LanceDataset
+    # over registered c2 fragments 436-475k img/s at depth 3 vs 297-308k at 2,
+    # two alternating registered c2 batches 389k at 3 vs 572-583k at 2;
+    # profiles/r4/dataset_depth_ab_r4dd.txt; a dataset loop asks for depth=3)
     pipe = DecodePipeline(depth=2 if auto else depth, device=device)
     image_column = fixed.get("image_column", "image")
     # depth=None: the options set on the first pipeline, replayed on the one
