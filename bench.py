@@ -211,7 +211,7 @@ def main():
     ap.add_argument("--dataset-epochs", type=int, default=2,
                     help="epochs in the dataset leg's timed region (each re-plans, as a training loop does)")
     ap.add_argument("--resize-impl", type=int, default=0,
-                    help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize4; 3 k_resize420 for 4:2:0)")
+                    help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize4; 1 its 32-bit 4:2:0 staging; 2 the streaming kernel)")
     ap.add_argument("--resize-waves-pct", type=int, default=0,
                     help="LDT_OPT_RESIZE_WAVES_PCT of every context (0: the library default, 100)")
     ap.add_argument("--resize-wg-waves", type=int, default=0,

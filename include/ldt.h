@@ -73,12 +73,7 @@ extern "C" {
                                  packed 16-bit pairs (k_resize4<5>); 1: the
                                  same with 32-bit upsampling (k_resize4<0>,
                                  round 3's default, cross-check); 2: the
-                                 streaming kernel for all (cross-check); 3: 4:2:0
-                                 sources <= 512 px wide two waves per band
-                                 (k_resize420, cross-check; slower); 4: the
-                                 same sources one staged row per step, 4 waves
-                                 per SIMD (k_resize4r, cross-check; no faster);
-                                 5: the packed 16-bit staging (as 0) */
+                                 streaming kernel for all (cross-check)        */
 #define LDT_OPT_SYNC_WARM 7   /* parallel decoder phase 1 starts this % of S
                                  before each range (0..200, default 0)         */
 #define LDT_OPT_COPY_THREADS 8 /* threads of the context's host copy pool that

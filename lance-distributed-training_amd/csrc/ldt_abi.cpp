@@ -200,6 +200,12 @@ int ensure_dev(ldt_ctx *c, DevBuf &b, size_t need, hipStream_t s, bool zero = fa
   if (b.p) {
     HIPCHK(c, hipStreamSynchronize(s));
     HIPCHK(c, hipDeviceSynchronize());
+    // the last batch's plan blob (ldt_debug_counters) may live in this buffer
+    const uintptr_t lo = (uintptr_t)b.p, lp = (uintptr_t)c->last_plan_dev;
+    if (lp >= lo && lp < lo + b.cap) {
+      c->last_plan_dev = nullptr;
+      c->last_off_redo = -1;
+    }
     HIPCHK(c, hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
@@ -957,9 +963,9 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.warm_pct = c->warm_pct;
   p.resize_waves_pct = c->resize_waves_pct;
   p.resize_wpg = c->resize_wpg;
-  // 4:2:0 sources <= 512 px: 0 / 5 the packed 16-bit staging (k_resize4<5>),
-  // 1 the 32-bit staging (k_resize4<0>), 3 k_resize420, 4 k_resize4r
-  p.resize420 = c->resize_impl == 3 ? 1 : (c->resize_impl == 4 ? 2 : (c->resize_impl == 1 ? 0 : 3));
+  // 4:2:0 sources <= 512 px: 0 the packed 16-bit staging (k_resize4<5>),
+  // 1 the 32-bit staging (k_resize4<0>)
+  p.resize420 = c->resize_impl == 1 ? 0 : 3;
   p.n_chunks = n_chunks;
   p.n_ds_img = n_ds_img;
   p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
@@ -991,9 +997,11 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_prog(p, w, s));
   HIPCHK(c, launch_dc_scan(p, w, s));
-  if (!data_dev) {
+  if (!data_dev && !plan_with_cells) {
     // the cells' last readers are enqueued: a later DMA into this slot's
-    // device buffer waits for them (copy stream)
+    // device buffer waits for them (copy stream). With the plan blob in the
+    // same buffer, its readers (k_idct, the resize, the status copy) come
+    // later: the event is recorded after the status copy below.
     HIPCHK(c, hipEventRecord(c->data_free_ev[sl], s));
     c->data_used[sl] = true;
   }
@@ -1029,6 +1037,12 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   }
   HIPCHK(c, hipMemcpyAsync(c->h_status[sl], w.status, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipEventRecord(c->st_ev[sl], s));
+  if (plan_with_cells) {
+    // every reader of the slot's device buffer (cells and plan blob) is
+    // enqueued: a later DMA into it waits for the status copy
+    HIPCHK(c, hipEventRecord(c->data_free_ev[sl], s));
+    c->data_used[sl] = true;
+  }
   c->st_ticket[sl] = ++c->tickets;
   c->st_n[sl] = n;
   c->last_sl = sl;
@@ -1174,7 +1188,7 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     c->warm_pct = (int)value;
     return LDT_OK;
   case LDT_OPT_RESIZE_IMPL:
-    if (value < 0 || value > 5) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
+    if (value < 0 || value > 2) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
     c->resize_impl = (int)value;
     return LDT_OK;
   case LDT_OPT_SUBSEQ_BITS:

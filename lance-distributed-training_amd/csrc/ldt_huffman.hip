@@ -31,14 +31,6 @@
 #include "ldt_device.hpp"
 #include "ldt_kernels.hpp"
 
-// The write pass's unit queue (see write_run): 2 units (the default: the
-// Huffman stage writes 166 MB per c2 batch instead of 235 MB unqueued, at the
-// same speed), 4 (-DLDT_EXP_WR_Q4: 132 MB, 2% slower c2) or none
-// (-DLDT_EXP_WR_Q1); profiles/r4/write_queue_ab_r4.txt.
-#if !defined(LDT_EXP_WR_Q1) && !defined(LDT_EXP_WR_Q4) && !defined(LDT_EXP_WR_NT)
-#define LDT_EXP_WR_Q2
-#endif
-
 namespace ldt {
 
 // LDS pointers keep their address space so loads compile to ds_read_* (a
@@ -398,24 +390,24 @@ struct RecGlob {
 // publishes its first unit as its chunk's carry. The loop has one group store
 // site: the buffered group is stored when a nonzero AC value opens another
 // group or a block starts.
+// Returns the symbols decoded (loop iterations; a diagnostic).
 template <class W, class RS>
-__device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
+__device__ __forceinline__ int write_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop,
                                           int &cursor, int lim, uint4 *__restrict__ coef_img,
                                           const RS &rs, int base) {
   uint64_t lo = 0, hi = 0;           // buffered group: slots 0-3, 4-7
   int cg = -1;                       // its group index; < 0: none
-#if defined(LDT_EXP_WR_Q2)
+  // units leave in pairs (one 32-byte store per two units: the Huffman stage
+  // writes 166 MB per c2 batch instead of 235 MB unpaired at the same speed;
+  // a 4-unit queue, 132 MB, cost 2%: profiles/r4/write_queue_ab_r4.txt)
   uint4 q2 = make_uint4(0u, 0u, 0u, 0u), q3 = q2;
-#elif defined(LDT_EXP_WR_Q4)
-  // a 4-unit queue: a run's units leave as whole 64-byte segments (a run
-  // starts at unit 8 x its first block, so unit 4i is 64-byte aligned)
-  uint4 q0 = make_uint4(0u, 0u, 0u, 0u), q1 = q0, q2 = q0;
-#endif
   uint32_t wu = (uint32_t)base * 8u; // units stored
   uint32_t gmask = 0;                // groups of the current block
   uint32_t dcd = 0;                  // its DC difference (16 bits)
   bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
+  int iters = 0;
   while (go) {
+    ++iters;
     R.refill();
     const bool first = st.k == 0; // a block starts: its DC symbol
     const uint32_t pk = R.peek();
@@ -429,7 +421,6 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
     const bool opens = !first && v != 0 && g != cg && cursor >= 0;
     const bool flush = cg >= 0 && (first || opens);
     const uint4 cur = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-#if defined(LDT_EXP_WR_Q2)
     if (flush) {
       q2 = q3;
       q3 = cur;
@@ -440,32 +431,6 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
         coef_img[wu - 1] = q3;
       }
     }
-#elif defined(LDT_EXP_WR_Q4)
-    if (flush) { // q0..q2 hold the segment's units so far (a shift register)
-      if ((wu & 3u) == 3u) {
-        coef_img[wu - 3] = q0;
-        coef_img[wu - 2] = q1;
-        coef_img[wu - 1] = q2;
-        coef_img[wu] = cur;
-      } else {
-        q0 = q1;
-        q1 = q2;
-        q2 = cur;
-      }
-      gmask |= 1u << cg;
-      ++wu;
-    }
-#else
-    if (flush) {
-#ifdef LDT_EXP_WR_NT
-      __builtin_nontemporal_store((v4u){cur.x, cur.y, cur.z, cur.w}, reinterpret_cast<v4u *>(coef_img + wu));
-#else
-      coef_img[wu] = cur;
-#endif
-      gmask |= 1u << cg;
-      ++wu;
-    }
-#endif
     // a block starts: the previous one's record, then this block's state
     if (first) {
       if (cursor >= 0) rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
@@ -488,43 +453,16 @@ __device__ __forceinline__ void write_run(Rd<W> &R, St &st, const Dec &dec, int3
   if (cursor >= 0) {
     if (cg >= 0) {
       const uint4 cur = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-#if defined(LDT_EXP_WR_Q2)
-      if (wu & 1u) {
-        coef_img[wu - 1] = q3;
-      }
-#endif
-#if defined(LDT_EXP_WR_Q4)
-      if ((wu & 3u) == 3u) {
-        coef_img[wu - 3] = q0;
-        coef_img[wu - 2] = q1;
-        coef_img[wu - 1] = q2;
-        coef_img[wu] = cur;
-      } else {
-        q0 = q1;
-        q1 = q2;
-        q2 = cur;
-      }
-#else
+      if (wu & 1u) coef_img[wu - 1] = q3;
       coef_img[wu] = cur;
-#endif
       gmask |= 1u << cg;
       ++wu;
-    }
-#if defined(LDT_EXP_WR_Q2)
-    else if (wu & 1u) {
+    } else if (wu & 1u) {
       coef_img[wu - 1] = q3;
     }
-#endif
-#if defined(LDT_EXP_WR_Q4)
-    { // the queue's pending units: the last n of q0..q2
-      const uint32_t n = wu & 3u, w0 = wu & ~3u;
-      if (n == 3u) coef_img[w0] = q0;
-      if (n >= 2u) coef_img[w0 + n - 2] = q1;
-      if (n >= 1u) coef_img[w0 + n - 1] = q2;
-    }
-#endif
     rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
   }
+  return iters;
 }
 
 // ---------------------------------------------------------------------------
@@ -1088,6 +1026,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   const int64_t nblk_img = (int64_t)d.mcux * d.mcuy * d.bpm;
   const bool rec_lds = nblk_img <= kRecCap;
   bool trunc = false;
+  int witers = 0;
   if (live) {
     // blocks of the segment started before this range: the first block whose
     // DC this range decodes is the segment's block `bstart`
@@ -1101,11 +1040,11 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     R.seek(g.pbias + wp);
     uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
     if (rec_lds)
-      write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
-                RecLds{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry}, base);
+      witers = write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
+                         RecLds{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry}, base);
     else
-      write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
-                RecGlob{brec + d.coef_off, bcarry + d.coef_off / 64}, base);
+      witers = write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
+                         RecGlob{brec + d.coef_off, bcarry + d.coef_off / 64}, base);
     if (g.j == sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;
@@ -1115,6 +1054,19 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   // publishes them to the other waves (one CU, one vector L1 and the LDS); an
   // agent-scope fence would write back and invalidate the XCD's whole L2.
   trunc = __syncthreads_or(trunc);
+  if (dbg) {
+    // write-pass symbols: summed over the lanes, and the waves' slowest lanes
+    int wsum = witers, wmax = witers;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      wsum += __shfl_xor(wsum, o);
+      wmax = max(wmax, __shfl_xor(wmax, o));
+    }
+    if ((tid & 63) == 0) {
+      atomicAdd(dbg + 5, wsum);
+      atomicAdd(dbg + 6, wmax);
+    }
+  }
   // diagnostic phase times (10 ns ticks summed over images; ldt_debug_counters)
   if (dbg && tid == 0) {
     const uint64_t t_end = wall_clock64();
@@ -1294,13 +1246,7 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   return true;
 }
 
-#if defined(LDT_EXP_WR_Q4) || defined(LDT_HUFF_WAVES4)
-// one 1024-lane workgroup per CU (its LDS): 4 waves per SIMD, up to 128 VGPRs
-#define LDT_HUFF_WPE __attribute__((amdgpu_waves_per_eu(4, 4)))
-#else
-#define LDT_HUFF_WPE
-#endif
-__global__ void __launch_bounds__(kHuffThreads) LDT_HUFF_WPE k_huff_image(
+__global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ data,
     const uint8_t *__restrict__ dstuf, const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,

@@ -37,7 +37,7 @@ struct DevPlan {
   int warm_pct;           // phase-1 warm-up before each range, % of S
   int resize_waves_pct;   // k_resize4 band count, % of one full wave of resize waves
   int resize_wpg;         // k_resize4 waves per workgroup for JPEG sources (0: default 2)
-  int resize420;          // 1: 4:2:0 images take k_resize420 (two waves per band); 2: k_resize4r (one staged row per step)
+  int resize420;          // 4:2:0 images <= 512 px: 3 k_resize4<5> (packed 16-bit staging), 0 k_resize4<0>
   int32_t *redo;          // debug counters of the parallel decoder (16 ints)
   int max_tabs;           // max distinct Huffman tables of one image (LDS slots)
   int n_fast420;         // images on k_resize4's fast staging path (resize_fast420)

@@ -237,10 +237,7 @@ constexpr int kResizeWaves = 2;
 // the waitcnt pass never sees another path's loads pending at the loop's
 // merge points (that forced a vmcnt(0) ahead of the horizontal taps and
 // serialised the prefetch).
-// SRC 4: the 4:2:0 fast path staging ONE source row per step (k_resize4r):
-// half the staging LDS and registers of SRC 0, so that a 2-wave workgroup
-// fits 20 KB and 4 waves per SIMD (128 VGPRs); the last horizontal job then
-// covers columns 192-223 with half the wave.
+// SRC 5: the 4:2:0 fast path on packed 16-bit pairs (the default).
 template <int SRC, int KS>
 __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
                                              const uint8_t *__restrict__ planes, RawSrc raw,
@@ -253,8 +250,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   // Skewed staging for raw rows (c5: 4-5-way tap conflicts otherwise, and the
   // kernel is LDS-bound). JPEG rows stay plain: the skew's extra registers
   // cost a wave per SIMD there, which is worth more than its 2-way conflicts.
-  constexpr bool kJpeg = SRC == 0 || SRC == 2 || SRC == 4 || SRC == 5;
-  constexpr bool kRow = SRC == 4; // one staged row per step
+  constexpr bool kJpeg = SRC == 0 || SRC == 2 || SRC == 5;
   constexpr bool kSkew = !kJpeg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
@@ -275,7 +271,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
       for (int i = lane; i < per; i += 64) o[c * (kOut * kOut / 4) + i] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
-  if (kJpeg && resize_fast420(descs[img]) != (SRC == 0 || SRC == 4 || SRC == 5)) return;
+  if (kJpeg && resize_fast420(descs[img]) != (SRC == 0 || SRC == 5)) return;
   int W, H;
   if constexpr (kJpeg) {
     W = descs[img].width;
@@ -290,8 +286,8 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   if (band == 0 && lane == 0 && labels != nullptr) out_labels[img] = labels[img];
 
   uint8_t *wbase = smem + 3072 + wave * g.wave_bytes;
-  uint32_t *stg = reinterpret_cast<uint32_t *>(wbase);               // 2 (kRow: 1) * spad dwords
-  uint8_t *ring = wbase + (kRow ? 4 : 8) * g.spad;                   // 3 * ring * 224
+  uint32_t *stg = reinterpret_cast<uint32_t *>(wbase);               // 2 * spad dwords
+  uint8_t *ring = wbase + 8 * g.spad;                                // 3 * ring * 224
   int32_t *kv = reinterpret_cast<int32_t *>(ring + 3 * g.ring * kOut); // kKvRows * ks_v
   int32_t *vb = kv + kKvRows * g.ks_v;                               // kKvRows * 2
   const int ks_v = g.ks_v, RING = g.ring;
@@ -326,7 +322,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
     ya = ymin_a;
     yb = ymin_b + cnt_b;
   }
-  const int ya0 = kJpeg && !kRow ? (ya & ~1) : ya;
+  const int ya0 = kJpeg ? (ya & ~1) : ya;
 
   // vertical-pass items: 168 dwords (3 channels x 56 groups of 4 columns)
   int vc[3], vo[3];
@@ -338,7 +334,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   }
 
   // JPEG fast path: 4:2:0 with both chroma planes fancy-upsampled, W <= 512
-  constexpr bool fast420 = SRC == 0 || SRC == 4 || SRC == 5;
+  constexpr bool fast420 = SRC == 0 || SRC == 5;
   constexpr bool kPk = SRC == 5; // packed 16-bit fancy upsampling
   int rc = 5, cdh = 1;
   // plane geometry copied to registers once: the wave fences in process()
@@ -373,21 +369,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   } pa;
   auto fetch = [&](Pre &pf, int y) {
     Jpair &jp = pf.jp;
-    if constexpr (kRow) {
-      // row y: 8 luma pixels, chroma rows cy and its fancy-upsampling
-      // neighbour (cy - 1 for an even row, cy + 1 for an odd one), 4 samples
-      const int x0 = lane * 8;
-      jp.y0 = x0 < W ? *reinterpret_cast<const uint2 *>(planes + po0 + (int64_t)y * ps0 + x0) : make_uint2(0, 0);
-      const int cy = y >> 1;
-      const int cn = (y & 1) ? min(cy + 1, cdh - 1) : max(cy - 1, 0);
-      const int cx0 = lane * 4;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const uint8_t *pc = planes + (c ? po2 : po1) + cx0;
-        jp.c[c][0] = cx0 < ps1 ? *reinterpret_cast<const uint32_t *>(pc + (int64_t)cy * ps1) : 0u;
-        jp.c[c][1] = cx0 < ps1 ? *reinterpret_cast<const uint32_t *>(pc + (int64_t)cn * ps1) : 0u;
-      }
-    } else if constexpr (kJpeg) {
+    if constexpr (kJpeg) {
       if constexpr (fast420) {
         const int x0 = lane * 8;
         const uint8_t *py = planes + po0 + (int64_t)y * ps0 + x0;
@@ -419,38 +401,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   auto stage = [&](const Pre &pf, int y) {
     const Jpair &jp = pf.jp;
     uint32_t *s0 = stg, *s1 = stg + g.spad;
-    if constexpr (kRow) {
-      // jdsample.c h2v2_fancy_upsample of row y (3 x the nearer chroma row +
-      // the farther one, then horizontally), jdcolor.c ycc_rgb_convert
-      const int x0 = lane * 8;
-      int up[2][8];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        int A[6], N[6], V[6];
-        bytes6(jp.c[c][0], lane, rc, A);
-        bytes6(jp.c[c][1], lane, rc, N);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) V[i] = A[i] * 3 + N[i];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int ci = (j >> 1) + 1;
-          const int nv = (j & 1) ? V[ci + 1] : V[ci - 1];
-          up[c][j] = (V[ci] * 3 + nv + 8 - (j & 1)) >> 4;
-        }
-      }
-      uint32_t px[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t yv = j < 4 ? jp.y0.x : jp.y0.y;
-        px[j] = ycc_px((int)((yv >> (8 * (j & 3))) & 255), up[0][j], up[1][j]);
-      }
-      if (x0 < W) {
-        uint4 *d0 = reinterpret_cast<uint4 *>(s0 + x0);
-        d0[0] = make_uint4(px[0], px[1], px[2], px[3]);
-        d0[1] = make_uint4(px[4], px[5], px[6], px[7]);
-      }
-      (void)s1;
-    } else if constexpr (kJpeg) {
+    if constexpr (kJpeg) {
       const ImgDesc &d = *dp;
       if constexpr (kPk) {
         // the same h2v2 fancy upsampling on packed 16-bit pairs: both output
@@ -579,11 +530,9 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   auto horizontal = [&](int y) {
     const int slot1 = slot + 1 == RING ? 0 : slot + 1;
 #pragma unroll
-    for (int job = 0; job < (kRow ? 4 : 7); ++job) {
-      // kRow: jobs q = 0..3 of the one row (q = 3: both half-waves compute
-      // columns 192-223 and store the same bytes)
-      const int q = kRow ? job : (job < 6 ? job >> 1 : 3);
-      const int r = kRow ? 0 : (job < 6 ? (job & 1) : (lane >> 5));
+    for (int job = 0; job < 7; ++job) {
+      const int q = job < 6 ? job >> 1 : 3;
+      const int r = job < 6 ? (job & 1) : (lane >> 5);
       const int ox = q < 3 ? lane + 64 * q : 192 + (lane & 31);
       const uint32_t *rowp = stg + (r ? g.spad : 0);
       int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
@@ -604,7 +553,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
       rw[RING * kOut] = (uint8_t)min((uint32_t)a1 >> kPrecisionBits, 255u);
       rw[2 * RING * kOut] = (uint8_t)min((uint32_t)a2 >> kPrecisionBits, 255u);
     }
-    slot = kRow ? slot1 : (slot1 + 1 == RING ? 0 : slot1 + 1);
+    slot = slot1 + 1 == RING ? 0 : slot1 + 1;
   };
   // finish every output row whose vertical window lies in ring rows [ya0, done)
   auto vertical = [&](int done) {
@@ -665,7 +614,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   // of being waited for (vmcnt counts loads and stores together) by the next
   // staging's wait for its prefetched rows. The ring size is unchanged: the
   // rows still pending need at most ks_v - 1 earlier rows plus this pair.
-  constexpr int kStep = kRow ? 1 : 2;
+  constexpr int kStep = 2;
   fetch(pa, ya0);
   for (int y = ya0; y < yb; y += kStep) {
     stage(pa, y);
@@ -689,278 +638,22 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
   resize4_body<SRC, KS>(descs, planes, raw, lut, labels, out, out_labels, status, g);
 }
 
-// the single-row 4:2:0 variant, held to 128 VGPRs (4 waves per SIMD)
-template <int KS>
-__global__ void __launch_bounds__(128, 4) k_resize4r(const ImgDesc *__restrict__ descs,
-                                                     const uint8_t *__restrict__ planes, RawSrc raw,
-                                                     const float *__restrict__ lut,
-                                                     const int64_t *__restrict__ labels,
-                                                     float *__restrict__ out,
-                                                     int64_t *__restrict__ out_labels,
-                                                     const int32_t *__restrict__ status, Geom4 g) {
-  resize4_body<4, KS>(descs, planes, raw, lut, labels, out, out_labels, status, g);
-}
-
-// ---------------------------------------------------------------------------
-// k_resize420 (LDT_OPT_RESIZE_IMPL 3; measured slower than k_resize4, see
-// DESIGN.md §4): the 4:2:0 fast path (resize_fast420 images) with TWO waves per
-// (image, band) task. Per source row pair the waves stage one row each (wave
-// w: row y + w, 8 luma pixels per lane, h2v2 fancy upsampling + YCbCr->RGB in
-// registers) into the workgroup's shared, skewed staging rows; after a
-// barrier each wave computes the horizontal taps of its own output columns
-// (wave 0: 0..127, wave 1: 128..223) for both rows into the ring and finishes
-// its own columns' output rows. Splitting the columns halves the weights a
-// lane keeps in registers and splitting the rows halves the staging
-// registers, which is what held k_resize4<0> to 3 waves per SIMD; the shared
-// staging costs two barriers per row pair between the two waves only.
-// ---------------------------------------------------------------------------
-struct GeomW2 {
-  int nbands, bh; // bands per image, output rows per band
-  int ring;       // intermediate ring rows (>= ks_v + 1)
-  int ks_v;       // vertical taps (max over the batch)
-  int spad;       // staging row stride in dwords (multiple of 4, skewed)
-  int ntask;      // n * nbands (one workgroup each)
-  int lds;        // LDS bytes per workgroup
-  int fill;       // this launch zero-fills failed images' bands (label -100)
-};
-
-template <int KS>
-__global__ void __launch_bounds__(128, 4) k_resize420(const ImgDesc *__restrict__ descs,
-                                                   const uint8_t *__restrict__ planes,
-                                                   const float *__restrict__ lut,
-                                                   const int64_t *__restrict__ labels,
-                                                   float *__restrict__ out,
-                                                   int64_t *__restrict__ out_labels,
-                                                   const int32_t *__restrict__ status, GeomW2 g) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  float *s_lut = reinterpret_cast<float *>(smem);
-  for (int i = tid; i < 768; i += 128) s_lut[i] = lut[i];
-  const int task = blockIdx.x;
-  const int img = task / g.nbands, band = task - img * g.nbands;
-  const int oy0 = band * g.bh, nb = min(g.bh, kOut - oy0);
-  if (status[img] != 0) {
-    // a failed image's band: zeros (and label -100), by one of the launches
-    if (!g.fill || nb <= 0) return;
-    if (band == 0 && tid == 0 && out_labels != nullptr) out_labels[img] = -100;
-    float4 *o = reinterpret_cast<float4 *>(out + (int64_t)img * 3 * kOut * kOut + oy0 * kOut);
-    const int per = nb * kOut / 4;
-    for (int c = 0; c < 3; ++c)
-      for (int i = tid; i < per; i += 128) o[c * (kOut * kOut / 4) + i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    return;
-  }
-  const ImgDesc &d = descs[img];
-  if (!resize_fast420(d) || nb <= 0) return;
-  const int W = d.width, H = d.height;
-  if (band == 0 && tid == 0 && labels != nullptr) out_labels[img] = labels[img];
-
-  uint32_t *stg = reinterpret_cast<uint32_t *>(smem + 3072);           // 2 rows of spad dwords
-  uint8_t *ring = smem + 3072 + 8 * g.spad;                            // 3 * ring * 224
-  const int kvb = 4 * (kKvRows * g.ks_v + 2 * kKvRows);                // per wave
-  int32_t *kv = reinterpret_cast<int32_t *>(ring + 3 * g.ring * kOut + wave * kvb);
-  int32_t *vb = kv + kKvRows * g.ks_v;
-  const int ks_v = g.ks_v, RING = g.ring;
-
-  // this wave's output columns: q = 0 -> c0 + lane; q = 1 -> c0 + 64 + lane
-  // (wave 0: both rows) or c0 + 64 + lane % 32 of row lane / 32 (wave 1)
-  const int c0 = wave * 128;
-  int32_t wgt[2][KS];
-  int xsk[2], xcr[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int ox = c0 + 64 * q + (q == 1 && wave == 1 ? (lane & 31) : lane);
-    int xm;
-    resample_coeffs_one(W, kOut, ox, KS, wgt[q], &xm);
-    xsk[q] = skw(xm);
-    xcr[q] = 32 - (xm & 31);
-  }
-  // band source rows
-  int ya, yb;
-  {
-    int32_t kk[32];
-    int ymin_a, ymin_b;
-    resample_coeffs_one(H, kOut, oy0, 0, kk, &ymin_a);
-    const int cnt_b = resample_coeffs_one(H, kOut, oy0 + nb - 1, 0, kk, &ymin_b);
-    ya = ymin_a;
-    yb = ymin_b + cnt_b;
-  }
-  const int ya0 = ya & ~1;
-  // vertical-pass items of this wave: dwords of 4 output columns, channel-major
-  const int cw4 = wave ? 24 : 32; // dwords per channel row (96 / 128 columns)
-  int vc[2], vo[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int it = min(lane + 64 * i, 3 * cw4 - 1);
-    vc[i] = it / cw4;
-    vo[i] = c0 + (it - vc[i] * cw4) * 4;
-  }
-  const int nvit = 3 * cw4;
-
-  const int dw = d.cdw[1];
-  const int rc = lane == (dw - 1) / 4 ? (dw - 1) % 4 + 1 : 5;
-  const int cdh = d.cdh[1];
-  const uint8_t *pY = planes + d.plane_off[0], *pCb = planes + d.plane_off[1], *pCr = planes + d.plane_off[2];
-  const int ps0 = d.plane_stride[0], ps1 = d.plane_stride[1];
-  const int x0 = lane * 8, cx0 = lane * 4;
-
-  // prefetched registers of this wave's row yy: 8 luma pixels, 4 chroma
-  // samples of rows cy and the fancy-upsampling neighbour row per component
-  uint2 py;
-  uint32_t pc[2][2]; // [Cb, Cr][row cy, neighbour]
-  auto fetch = [&](int yy) {
-    py = (x0 < W && yy < H) ? *reinterpret_cast<const uint2 *>(pY + (int64_t)yy * ps0 + x0) : make_uint2(0, 0);
-    const int cy = yy >> 1;
-    const int cn = wave == 0 ? max(cy - 1, 0) : min(cy + 1, cdh - 1);
-    const int ca = min(cy, cdh - 1);
-    const bool ok = cx0 < ps1;
-    pc[0][0] = ok ? *reinterpret_cast<const uint32_t *>(pCb + (int64_t)ca * ps1 + cx0) : 0u;
-    pc[0][1] = ok ? *reinterpret_cast<const uint32_t *>(pCb + (int64_t)cn * ps1 + cx0) : 0u;
-    pc[1][0] = ok ? *reinterpret_cast<const uint32_t *>(pCr + (int64_t)ca * ps1 + cx0) : 0u;
-    pc[1][1] = ok ? *reinterpret_cast<const uint32_t *>(pCr + (int64_t)cn * ps1 + cx0) : 0u;
-  };
-  // jdsample.c h2v2_fancy_upsample for this wave's row (even rows take the
-  // row above as neighbour, odd rows the row below), jdcolor.c ycc_rgb_convert
-  auto stage = [&]() {
-    int up[2][8];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      int A[6], N[6];
-      bytes6(pc[c][0], lane, rc, A);
-      bytes6(pc[c][1], lane, rc, N);
-      int V[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) V[i] = A[i] * 3 + N[i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int ci = (j >> 1) + 1;
-        const int nv = (j & 1) ? V[ci + 1] : V[ci - 1];
-        up[c][j] = (V[ci] * 3 + nv + 8 - (j & 1)) >> 4;
-      }
-    }
-    uint32_t p[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t yv = j < 4 ? py.x : py.y;
-      p[j] = ycc_px((int)((yv >> (8 * (j & 3))) & 255), up[0][j], up[1][j]);
-    }
-    if (x0 < W) {
-      uint4 *dd = reinterpret_cast<uint4 *>(stg + wave * g.spad + skw(x0));
-      dd[0] = make_uint4(p[0], p[1], p[2], p[3]);
-      dd[1] = make_uint4(p[4], p[5], p[6], p[7]);
-    }
-  };
-
-  int next_oy = 0, kv_base = -1, slot = 0;
-  auto horizontal = [&]() {
-    const int slot1 = slot + 1 == RING ? 0 : slot + 1;
-#pragma unroll
-    for (int job = 0; job < 4; ++job) {
-      if (wave == 1 && job == 3) break; // wave 1: 96 columns = 3 jobs
-      const int q = job >> 1;
-      const int r = (q == 1 && wave == 1) ? (lane >> 5) : (job & 1);
-      const int ox = c0 + 64 * q + (q == 1 && wave == 1 ? (lane & 31) : lane);
-      const uint32_t *rowp = stg + (r ? g.spad : 0);
-      int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
-#pragma unroll
-      for (int t = 0; t < KS; ++t) {
-        // the window crosses at most one 32-pixel skew step, at tap xcr[q]
-        const uint32_t v = (rowp + (t < xcr[q] ? xsk[q] : xsk[q] + 4))[t];
-        const uint32_t kw = (uint32_t)wgt[q][t];
-        a0 += (int32_t)__umul24(v & 255, kw);
-        a1 += (int32_t)__umul24((v >> 8) & 255, kw);
-        a2 += (int32_t)__umul24((v >> 16) & 255, kw);
-      }
-      uint8_t *rw = ring + (r ? slot1 : slot) * kOut + ox;
-      rw[0] = (uint8_t)min((uint32_t)a0 >> kPrecisionBits, 255u);
-      rw[RING * kOut] = (uint8_t)min((uint32_t)a1 >> kPrecisionBits, 255u);
-      rw[2 * RING * kOut] = (uint8_t)min((uint32_t)a2 >> kPrecisionBits, 255u);
-    }
-    slot = slot1 + 1 == RING ? 0 : slot1 + 1;
-  };
-  // finish this wave's columns of every output row whose vertical window lies
-  // in ring rows [ya0, done)
-  auto vertical = [&](int done) {
-    while (next_oy < nb) {
-      const int j = next_oy;
-      if (j >= kv_base + kKvRows || kv_base < 0) {
-        kv_base = j;
-        if (lane < kKvRows && j + lane < nb) {
-          int ymin;
-          const int cnt = resample_coeffs_one(H, kOut, oy0 + j + lane, ks_v, kv + lane * ks_v, &ymin);
-          vb[2 * lane] = ymin;
-          vb[2 * lane + 1] = cnt;
-        }
-        wave_lds_fence();
-      }
-      const int jr = j - kv_base;
-      const int ymin = __builtin_amdgcn_readfirstlane(vb[2 * jr]);
-      const int cnt = __builtin_amdgcn_readfirstlane(vb[2 * jr + 1]);
-      if (ymin + cnt > done) break;
-      ++next_oy;
-      const int s0 = (ymin - ya0) % RING;
-      int32_t acc[2][4];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][e] = 1 << (kPrecisionBits - 1);
-      for (int t = 0; t < cnt; ++t) {
-        const uint32_t kw = (uint32_t)__builtin_amdgcn_readfirstlane(kv[jr * ks_v + t]);
-        const int sl = s0 + t < RING ? s0 + t : s0 + t - RING;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const uint32_t v = *reinterpret_cast<const uint32_t *>(ring + (vc[i] * RING + sl) * kOut + vo[i]);
-          acc[i][0] += (int32_t)__umul24(v & 255, kw);
-          acc[i][1] += (int32_t)__umul24((v >> 8) & 255, kw);
-          acc[i][2] += (int32_t)__umul24((v >> 16) & 255, kw);
-          acc[i][3] += (int32_t)__umul24(v >> 24, kw);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (lane + 64 * i < nvit) {
-          const float *lc = s_lut + vc[i] * 256;
-          float4 f;
-          f.x = lc[min((uint32_t)acc[i][0] >> kPrecisionBits, 255u)];
-          f.y = lc[min((uint32_t)acc[i][1] >> kPrecisionBits, 255u)];
-          f.z = lc[min((uint32_t)acc[i][2] >> kPrecisionBits, 255u)];
-          f.w = lc[min((uint32_t)acc[i][3] >> kPrecisionBits, 255u)];
-          *reinterpret_cast<float4 *>(out + (((int64_t)img * 3 + vc[i]) * kOut + oy0 + j) * kOut + vo[i]) = f;
-        }
-      }
-    }
-  };
-
-  fetch(ya0 + wave);
-  __syncthreads(); // the LUT
-  for (int y = ya0; y < yb; y += 2) {
-    stage();
-    if (y + 2 < yb) fetch(y + 2 + wave);
-    __syncthreads(); // both staged rows visible
-    vertical(y);
-    horizontal();
-    __syncthreads(); // every read of the staging rows done before they are rewritten
-  }
-  vertical(yb + 1);
-}
-
 // ---------------------------------------------------------------------------
 // Launch geometry.
 // ---------------------------------------------------------------------------
-static int wave_bytes4(const Geom4 &g, int rows) {
-  const int b = 4 * rows * g.spad + 3 * g.ring * kOut + 4 * (kKvRows * g.ks_v + 2 * kKvRows);
+static int wave_bytes4(const Geom4 &g) {
+  const int b = 8 * g.spad + 3 * g.ring * kOut + 4 * (kKvRows * g.ks_v + 2 * kKvRows);
   return (b + 15) & ~15;
 }
 
-// rows: staged source rows per step (2; 1 for the single-row 4:2:0 kernel)
-static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g, int rows = 2,
+static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g,
                        int wpg = kResizeWaves) {
   g.wpg = wpg;
   g.ks_v = resample_ksize_host(max_h, kOut);
   g.ring = g.ks_v + 1; // an output row is finished within 2 rows of its window end
   const int px = ((max_w + 15) / 16) * 16 + ks_h + 16;
   g.spad = (px + ((px >> 5) << 2) + 4 + 3) & ~3; // skewed pixels (skw)
-  g.wave_bytes = wave_bytes4(g, rows);
+  g.wave_bytes = wave_bytes4(g);
   int nb = (waves_target + n - 1) / n;
   if (nb < 1) nb = 1;
   if (nb > 28) nb = 28;
@@ -998,21 +691,8 @@ static bool dispatch4(int ks_h, const ImgDesc *descs, const uint8_t *planes, Raw
   }
 }
 
-template <int KS>
-static hipError_t launch4r(const ImgDesc *descs, const uint8_t *planes, const float *lut, const int64_t *labels,
-                           float *out, int64_t *out_labels, const int32_t *status, const Geom4 &g, hipStream_t s) {
-  static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resize4r<KS>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (attr != hipSuccess) return attr;
-  const int groups = (g.ntask + kResizeWaves - 1) / kResizeWaves;
-  hipLaunchKernelGGL((k_resize4r<KS>), dim3(groups), dim3(64 * kResizeWaves), 3072 + kResizeWaves * g.wave_bytes,
-                     s, descs, planes, RawSrc{nullptr, 0, 0, 0}, lut, labels, out, out_labels, status, g);
-  return hipGetLastError();
-}
-
 // Waves to aim for: the CU count times the resident waves per CU the LDS
-// allows (at most 12; 16 for the single-row kernel, whose workgroups fit 8
-// per CU).
+// allows (at most 12).
 static int waves_target4(const Geom4 &g, int pct, int max_waves = 12) {
   const int max_wg = max_waves / g.wpg;
   static int cus = 0;
@@ -1030,96 +710,26 @@ static int waves_target4(const Geom4 &g, int pct, int max_waves = 12) {
   return cus * g.wpg * wg * (pct > 0 ? pct : 100) / 100;
 }
 
-static int cu_count() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) cus = 256;
-    else cus = prop.multiProcessorCount;
-  }
-  return cus;
-}
-
-// k_resize420 geometry: bands so that the batch's workgroups fill the GPU
-// about once (`pct` % of the resident workgroups), at most 28 per image.
-static bool make_geom_w2(int n, int max_w, int max_h, int ks_h, int pct, GeomW2 &g) {
-  g.ks_v = resample_ksize_host(max_h, kOut);
-  g.ring = g.ks_v + 1;
-  const int px = ((max_w + 15) / 16) * 16 + ks_h + 16;
-  g.spad = (px + ((px >> 5) << 2) + 4 + 3) & ~3;
-  g.lds = 3072 + 8 * g.spad + 3 * g.ring * kOut + 2 * 4 * (kKvRows * g.ks_v + 2 * kKvRows);
-  g.lds = (g.lds + 15) & ~15;
-  if (g.lds > 64 * 1024) return false;
-  int wg_cu = (160 * 1024) / g.lds;
-  if (wg_cu > 8) wg_cu = 8; // 16 waves per CU: what the registers allow
-  const int target = cu_count() * wg_cu * (pct > 0 ? pct : 100) / 100;
-  int nb = (target + n - 1) / n;
-  if (nb < 1) nb = 1;
-  if (nb > 28) nb = 28;
-  g.bh = (kOut + nb - 1) / nb;
-  g.nbands = (kOut + g.bh - 1) / g.bh;
-  g.ntask = n * g.nbands;
-  g.fill = 1;
-  return true;
-}
-
-template <int KS>
-static hipError_t launch_w2(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
-                            const GeomW2 &g, hipStream_t s) {
-  hipLaunchKernelGGL((k_resize420<KS>), dim3(g.ntask), dim3(128), g.lds, s, p.descs, w.planes, p.lut,
-                     p.labels, out, out_labels, w.status, g);
-  return hipGetLastError();
-}
-
 bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
                          hipStream_t s, hipError_t *err) {
   Geom4 g;
   const int ks_h = resample_ksize_host(p.max_w, kOut);
   if (ks_h > 11) return false;
   const int wpg = p.resize_wpg > 0 ? p.resize_wpg : kResizeWaves;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, 2, wpg)) return false;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g, 2, wpg)) return false;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, wpg)) return false;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g, wpg)) return false;
   RawSrc raw{nullptr, 0, 0, 0};
   // fast-path images and the rest go to separate kernels (each skips the
   // other's images); a batch of one kind launches one kernel. The first
   // launch also writes the failed images (k_fill_failed's job otherwise).
   g.fill = 1;
-  if (p.n_fast420 > 0 && p.resize420 == 2) {
-    // single-row 4:2:0 kernel (LDT_OPT_RESIZE_IMPL 4), W <= 512
-    Geom4 gr;
-    const int ks_f = resample_ksize_host(std::min(p.max_w, 512), kOut);
-    if (ks_f <= 7 && make_geom4(p.n, std::min(p.max_w, 512), p.max_h, ks_f, 1, gr, 1) &&
-        make_geom4(p.n, std::min(p.max_w, 512), p.max_h, ks_f, waves_target4(gr, p.resize_waves_pct, 16), gr, 1)) {
-      gr.fill = 1;
-      switch (ks_f) {
-      case 3: *err = launch4r<3>(p.descs, w.planes, p.lut, p.labels, out, out_labels, w.status, gr, s); break;
-      case 5: *err = launch4r<5>(p.descs, w.planes, p.lut, p.labels, out, out_labels, w.status, gr, s); break;
-      default: *err = launch4r<7>(p.descs, w.planes, p.lut, p.labels, out, out_labels, w.status, gr, s); break;
-      }
-      if (*err != hipSuccess || p.n_fast420 == p.n) return true;
-      g.fill = 0;
-      return dispatch4<2>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s, err);
-    }
-  }
   if (p.n_fast420 > 0) {
-    GeomW2 g2;
-    const int ks_f = resample_ksize_host(std::min(p.max_w, 512), kOut);
-    if (p.resize420 == 1 && make_geom_w2(p.n, std::min(p.max_w, 512), p.max_h, ks_f, p.resize_waves_pct, g2) &&
-        ks_f <= 7) {
-      // 4:2:0 images (width <= 512): two waves per band
-      switch (ks_f) {
-      case 3: *err = launch_w2<3>(p, w, out, out_labels, g2, s); break;
-      case 5: *err = launch_w2<5>(p, w, out, out_labels, g2, s); break;
-      default: *err = launch_w2<7>(p, w, out, out_labels, g2, s); break;
-      }
-    } else if (p.resize420 == 3) {
-      if (!dispatch4<5>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s, err))
-        return false;
-    } else if (!dispatch4<0>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s,
-                             err)) {
-      return false;
-    }
+    // 4:2:0 images of width <= 512: the packed 16-bit staging (k_resize4<5>),
+    // or the 32-bit one (k_resize4<0>, LDT_OPT_RESIZE_IMPL 1, cross-check)
+    const bool ok = p.resize420 == 3
+                        ? dispatch4<5>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s, err)
+                        : dispatch4<0>(ks_h, p.descs, w.planes, raw, p.lut, p.labels, out, out_labels, w.status, g, s, err);
+    if (!ok) return false;
     if (*err != hipSuccess || p.n_fast420 == p.n) return true;
     g.fill = 0;
   }

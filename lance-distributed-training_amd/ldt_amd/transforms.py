@@ -795,15 +795,20 @@ def _cell_bytes(batch, col: str) -> int:
     try:
         if col not in batch.schema.names:
             return 0
-        arr = _column(batch, col)
-        if isinstance(arr, pa.ChunkedArray):
-            arr = arr.combine_chunks()
-        off = arr.buffers()[1]
-        if pa.types.is_fixed_size_binary(arr.type):
-            return len(arr) * arr.type.byte_width
-        dt = np.int64 if pa.types.is_large_binary(arr.type) else np.int32
-        o = np.frombuffer(off, dtype=dt)
-        return int(o[arr.offset + len(arr)] - o[arr.offset])
+        col_ = batch.column(col)  # a Table's column stays chunked here
+        # a chunked column: the chunks' byte spans summed (no combine_chunks copy)
+        chunks = col_.chunks if isinstance(col_, pa.ChunkedArray) else [col_]
+        tot = 0
+        for arr in chunks:
+            if pa.types.is_fixed_size_binary(arr.type):
+                tot += len(arr) * arr.type.byte_width
+                continue
+            if len(arr) == 0:
+                continue
+            dt = np.int64 if pa.types.is_large_binary(arr.type) else np.int32
+            o = np.frombuffer(arr.buffers()[1], dtype=dt)
+            tot += int(o[arr.offset + len(arr)] - o[arr.offset])
+        return tot
     except Exception:  # not a host binary column: keep the default
         return 0
 
@@ -825,8 +830,9 @@ def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, 
 
     ``depth=None``: chosen at the first call from its batch, 3 for batches of
     fewer than 8 MB of encoded cells (FOOD101-shaped batches of 128), else 2
-    (``auto_host_depth``); options set through ``fn.pipeline`` before that
-    call carry over. The ``fn.iterate`` (prefetch) path keeps depth 2. A
+    (``auto_host_depth``); options set through ``fn.pipeline.set_option``
+    before that call carry over (options set on one of its contexts,
+    ``fn.pipeline.ctxs[i]``, do not: the first call may replace the pipeline). The ``fn.iterate`` (prefetch) path keeps depth 2. A
     ``LanceDataset`` loop over registered (mapped) fragments should ask for
     ``depth=3``.
 
@@ -870,9 +876,11 @@ def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, 
     # must not evict on every call; `evictions` holds the call numbers of the
     # recent evictions
     calls = [0]
+    seen = [0]  # batches offered to maybe_register (to_tensor_fn and the fn.iterate path)
     evictions: list = []
 
     def maybe_register(batch, col):
+        seen[0] += 1
         if not reg_on[0] or not isinstance(batch, pa.RecordBatch):
             return
         arr = _column(batch, col)
@@ -894,11 +902,11 @@ def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, 
         while len(owned) > cap:
             _, old = owned.popitem(last=False)
             unregister_host(old)
-            evictions.append(calls[0])
-        # more evictions than the cap within 4 x cap calls: the buffers do not
+            evictions.append(seen[0])
+        # more evictions than the cap within 4 x cap batches: the buffers do not
         # repeat, so registration cannot amortise; the copying path from here
         # on (the ranges still registered are released at once)
-        while evictions and evictions[0] < calls[0] - 4 * cap:
+        while evictions and evictions[0] < seen[0] - 4 * cap:
             evictions.pop(0)
         if len(evictions) > cap:
             reg_on[0] = False

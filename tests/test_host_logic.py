@@ -205,3 +205,70 @@ def test_auto_host_depth_from_cell_bytes():
     fx = pa.RecordBatch.from_arrays([pa.array([b"x" * 48] * 9, pa.binary(48))], names=["image"])
     assert _cell_bytes(fx.slice(2, 5), "image") == 5 * 48
     assert _cell_bytes(fx, "missing") == 0
+    # a Table's chunked column: the chunks' spans, no combine
+    tb = pa.Table.from_batches([pa.RecordBatch.from_arrays([pa.array(cells[:15], pa.binary())], names=["image"]),
+                                pa.RecordBatch.from_arrays([pa.array(cells[15:], pa.binary())], names=["image"])])
+    assert tb.column("image").num_chunks == 2
+    assert _cell_bytes(tb, "image") == sum(map(len, cells))
+
+
+class _FakePipeline:
+    """DecodePipeline stand-in for host-logic tests (no GPU): records decodes."""
+
+    def __init__(self, depth=2, device=None, profile=False):
+        self.depth = depth
+        self.k = 0
+        self.ctxs = []
+
+    def set_option(self, opt, value):
+        pass
+
+    def check_slot(self, i):
+        pass
+
+    def check(self):
+        pass
+
+    def decode(self, batch, **kw):
+        self.k += 1
+        return None, None
+
+    def prefetch(self, batches, ahead=2, **kw):
+        for b in batches:
+            self.k += 1
+            yield {"image": b}
+
+
+def test_register_churn_guard_counts_prefetch_batches(monkeypatch):
+    """make_to_tensor_fn(register=True): the churn guard counts batches on the
+    fn.iterate (prefetch) path too, so a loop cycling over more mapped buffers
+    than register_cap, each serving many batches, keeps registering (ADVICE r4:
+    the guard's window never slid on that path and switched registration off
+    after cap+1 evictions), while buffers that never repeat switch it off."""
+    from ldt_amd import transforms as T
+
+    regs = []
+    monkeypatch.setattr(T, "DecodePipeline", _FakePipeline)
+    monkeypatch.setattr(T, "register_host", lambda arr, device=None: regs.append(T._host_range(arr)[0]))
+    monkeypatch.setattr(T, "unregister_host", lambda arr: None)
+    monkeypatch.setattr(T, "_as_device_batch", lambda img, lbl: {"image": img})
+    frags = [pa.RecordBatch.from_arrays([pa.array([bytes([f]) * 64] * 400, pa.binary())], names=["image"])
+             for f in range(5)]
+    # 5 fragments, cap 2: every fragment change evicts, but each serves 20 batches
+    order = [frags[(k // 20) % 5].slice((k % 20) * 10, 10) for k in range(400)]
+    for use_iterate in (True, False):
+        regs.clear()
+        fn = T.make_to_tensor_fn(depth=2, register=True, register_cap=2, prefetch=1)
+        if use_iterate:
+            assert sum(1 for _ in fn.iterate(order)) == 400
+        else:
+            for b in order:
+                fn(b)
+        assert fn.registering(), use_iterate
+        assert len(regs) == 20  # one registration per fragment visit
+    # fresh buffers every batch: no reuse, registration switches off
+    fn = T.make_to_tensor_fn(depth=2, register=True, register_cap=2, prefetch=1)
+    fresh = [pa.RecordBatch.from_arrays([pa.array([bytes([k % 251]) * 64] * 10, pa.binary())], names=["image"])
+             for k in range(40)]
+    assert sum(1 for _ in fn.iterate(fresh)) == 40
+    assert not fn.registering()

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes (one rocprofv3 run per counter group) of tests/probe_resize.py <mode>.
+# PMC passes (one rocprofv3 run per counter group) of tools/probes/probe_resize.py <mode> (PROBE=<file in tools/probes>).
 # Stops at the first failed pass. usage: bash tools/pmc.sh <tag> <mode> [pass numbers]
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/pmc_$1
@@ -15,7 +15,7 @@ PASSES=${*:3}
 PASSES=${PASSES:-"1 2 3 4 5"}
 for i in $PASSES; do
   ctrs=${GROUPS_[$((i-1))]}
-  timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $R/gpurun_out/pmc_$1/p$i -o run -- python3 $R/tests/${PROBE:-probe_resize.py} $2 > $R/gpurun_out/pmc_$1/p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $R/gpurun_out/pmc_$1/p$i -o run -- python3 $R/tools/probes/${PROBE:-probe_resize.py} $2 > $R/gpurun_out/pmc_$1/p$i.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "pass $i failed rc=$rc"; tail -5 $R/gpurun_out/pmc_$1/p$i.log; exit $rc; fi
 done

@@ -10,7 +10,7 @@ import ldt_amd  # noqa: E402
 from ldt_amd import _lib, synth  # noqa: E402
 
 ctx = _lib.get_context(0)
-names = ["redo", "wgs", "rounds_sum", "rounds_max", "memo_hits", "walk_first", "walk_steps", "fallbacks",
+names = ["redo", "wgs", "rounds_sum", "rounds_max", "memo_hits", "write_syms", "write_wave_max", "fallbacks",
          "t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "need_lanes", "need_waves", "t_dc_idct"]
 for wl, fn, n in (("c2", synth.q90_512, 256), ("c1", synth.food101_like, 128), ("c4", synth.imagenet_like, 128)):
     cells, labels = fn(n, seed=1000)
@@ -25,4 +25,8 @@ for wl, fn, n in (("c2", synth.q90_512, 256), ("c1", synth.food101_like, 128), (
         d[k + "_us"] = round(d.pop(k) / w / 100.0, 2)  # 10 ns ticks per image
     d["need_lanes_per_round"] = round(d["need_lanes"] / max(d["rounds_sum"], 1), 1)
     d["need_waves_per_round"] = round(d["need_waves"] / max(d["rounds_sum"], 1), 2)
+    # write pass: symbols per image, per lane, and the slowest lane of each wave
+    d["write_syms_per_img"] = round(d["write_syms"] / w, 1)
+    d["write_syms_per_lane"] = round(d["write_syms"] / w / 1024, 2)
+    d["write_wave_max_per_lane"] = round(d["write_wave_max"] / w / 16, 2)
     print(wl, d, flush=True)

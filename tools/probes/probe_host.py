@@ -1,6 +1,6 @@
 """Diagnostic (not a test): host wall time per DecodePipeline.decode call."""
 import os, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "lance-distributed-training_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "lance-distributed-training_amd"))
 import numpy as np, torch, ldt_amd
 from ldt_amd import synth
 dev = torch.device("cuda", 0)

@@ -1,13 +1,13 @@
 """Diagnostic (not a test): per-image max abs diff vs the oracle for both
 resize implementations on the golden images and config batches."""
 import json, os, sys
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "lance-distributed-training_amd"))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "lance-distributed-training_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 import numpy as np, pyarrow as pa
 import ldt_amd
 from ldt_amd import _lib, synth
 from oracle import oracle
-G = os.path.join(os.path.dirname(__file__), "golden")
+G = os.path.join(os.path.dirname(__file__), "..", "..", "tests", "golden")
 man = json.load(open(os.path.join(G, "manifest.json")))
 ctx = _lib.get_context(0)
 def batch(cells):

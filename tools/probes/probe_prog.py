@@ -3,7 +3,7 @@ for PMC/kernel-trace runs of k_prog. GPU box only."""
 import os
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "lance-distributed-training_amd"))
 import torch  # noqa: E402
 

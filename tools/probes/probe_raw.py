@@ -1,8 +1,8 @@
 """Diagnostic: raw resize diff pattern vs the oracle."""
 import os, sys
 import numpy as np
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "lance-distributed-training_amd"))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "lance-distributed-training_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 import torch, ldt_amd
 from oracle import oracle
 for (h, w) in ((300, 200), (224, 224), (40, 1000), (1024, 1024), (500, 333)):

@@ -1,6 +1,6 @@
 """Diagnostic (not a test): run the resize kernels alone for PMC profiling."""
 import os, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "lance-distributed-training_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "lance-distributed-training_amd"))
 import torch, ldt_amd
 from ldt_amd import synth
 which = sys.argv[1] if len(sys.argv) > 1 else "raw"

@@ -1,6 +1,6 @@
 """Diagnostic (not a test): parallel Huffman sync statistics per workload."""
 import sys, os, numpy as np
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "lance-distributed-training_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "lance-distributed-training_amd"))
 import torch, ldt_amd
 from ldt_amd import _lib, synth
 ctx = _lib.get_context(0)
