@@ -206,8 +206,9 @@ def main():
     ap.add_argument("--depth", type=int, default=None,
                     help="batches in flight (ldt_amd.DecodePipeline: one context + HIP stream each); default 3, "
                          "7 for progressive workloads (a c2p batch takes ~13 ms on the device)")
-    ap.add_argument("--dataset-batches", type=int, default=12,
-                    help="batches per rank of one epoch of the dataset leg (0: skip the leg)")
+    ap.add_argument("--dataset-batches", type=int, default=100,
+                    help="batches per rank of one epoch of the dataset legs at N=1 (divided by the world size, at "
+                         "least 12, so that the dataset rank 0 writes stays the same size; 0: skip the legs)")
     ap.add_argument("--dataset-epochs", type=int, default=2,
                     help="epochs in the dataset leg's timed region (each re-plans, as a training loop does)")
     ap.add_argument("--resize-impl", type=int, default=0,
@@ -239,6 +240,8 @@ def main():
     ap.add_argument("--dataset-copy", action="store_true",
                     help="dataset legs through the copying to_tensor_fn instead of registering the mapped "
                          "fragments' image buffers")
+    ap.add_argument("--no-workload-legs", action="store_true",
+                    help="skip the configs[4] (c5) and progressive (c2p) legs of a c2 run")
     args = ap.parse_args()
     progressive = args.workload.endswith("p")
     # progressive batches spend ~13 ms in k_prog: 7 in flight (4 slots on
@@ -444,11 +447,18 @@ def main():
         else:
             host_ranks = [mine]
 
-    value_dataset = None
-    dataset_info = None
+    value_dataset = value_dataset_copy = None
+    dataset_info = dataset_copy_info = None
     if args.workload != "c5" and args.dataset_batches > 0:
         value_dataset, dataset_info = dataset_rate(args, wl, B, world, rank, dev, cells_all, labels_all,
-                                                   barrier, max_over_ranks)
+                                                   barrier, max_over_ranks, keep=not args.dataset_copy)
+        if not args.dataset_copy:
+            # pylance hands to_tensor_fn a fresh RecordBatch per read
+            # (lance_iterable.py:38-41, :53-59): the copying to_tensor_fn at its
+            # own depth, as a loop that cannot register its buffers runs it
+            value_dataset_copy, dataset_copy_info = dataset_rate(args, wl, B, world, rank, dev, cells_all,
+                                                                 labels_all, barrier, max_over_ranks,
+                                                                 copy=True)
     # BASELINE configs[2] (c3) and configs[3] (c4) as written — the reference's
     # iterable loop over FOOD101-shaped / ImageNet-shaped cells with its own
     # sampler — in the same run as the headline, so that every N of a scaling
@@ -487,6 +497,17 @@ def main():
 
     # measured HBM ceiling on this box, after the timed region
     ceiling = stream_copy_ceiling(dev)
+
+    # configs[4] (c5: raw 1024^2 -> 224 + Normalize, the HBM-roofline stress)
+    # and the progressive path (c2p) in the same run as the headline, each
+    # with its own roofline / host-input / CPU figures (the driver runs only
+    # the default command)
+    workload_legs = {}
+    if args.workload == "c2" and not args.only_resident and not args.no_workload_legs:
+        cpu_ok = rank == 0 and world == 1 and not args.no_cpu_baseline
+        workload_legs["c5"] = leg_c5(args, dev, world, rank, barrier, max_over_ranks, cpu_ok)
+        workload_legs["c2p"] = leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok)
+
 
     # roofline: the resize/normalise stage (north_star), from live HIP events
     rs_ms, rs_n = stages["resize"]
@@ -552,6 +573,12 @@ def main():
         res["value_dataset"] = round(value_dataset, 1)
         res["value_dataset_per_gpu"] = round(value_dataset / world, 1)
         res["dataset_leg"] = dataset_info
+    if value_dataset_copy is not None:
+        res["value_dataset_copy"] = round(value_dataset_copy, 1)
+        res["value_dataset_copy_per_gpu"] = round(value_dataset_copy / world, 1)
+        res["dataset_copy_leg"] = dataset_copy_info
+    if workload_legs:
+        res["workload_legs"] = workload_legs
     if standalone is not None:
         sa_ms, sa_n = standalone["resize"]
         sa_s = sa_ms / max(sa_n, 1) / 1e3
@@ -594,7 +621,8 @@ def main():
         dist.destroy_process_group()
 
 
-def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over_ranks, tag=None):
+def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over_ranks, tag=None, copy=None,
+                 keep=False):
     """The reference's iterable loop (lance_iterable.py:53-72, :86-116) over an
     Arrow/Lance dataset of this workload's cells: LanceDataset + the sampler +
     the pipelined to_tensor_fn, `dataset_epochs` full epochs per rank in the
@@ -603,7 +631,10 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     dataset (the workload's cells repeated to `dataset_batches` batches per
     rank) into fragments of the config's shape; every rank then runs one
     untimed epoch and the timed ones. Padding batches (pad=True) are decoded
-    and counted. Returns (whole-job img/s, info)."""
+    and counted. `copy` (default --dataset-copy): the copying to_tensor_fn at
+    make_to_tensor_fn's own depth instead of registered fragments at
+    --dataset-depth. `keep`: leave the dataset for the next leg over the same
+    cells (it is then not written again). Returns (whole-job img/s, info)."""
     import shutil
 
     import numpy as np
@@ -612,7 +643,10 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     import ldt_amd
     from ldt_amd import _lib
 
-    nbatch = args.dataset_batches
+    copy = args.dataset_copy if copy is None else copy
+    # the dataset rank 0 writes holds every rank's rows: per-rank batches
+    # shrink with the world size (at least 12) so that it stays ~1.7 GB at c2
+    nbatch = max(12, args.dataset_batches // world)
     # FOOD101's fragments [12500 x 6, 750] (create_datasets/classification.py:16,60)
     # scaled so that a rank reads about `nbatch` batches
     if wl["sampler"] == "fragment":
@@ -630,7 +664,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
 
     path = os.path.join(tempfile.gettempdir(),
                         f"ldt_bench_ds_{os.environ.get('MASTER_PORT', '0')}_{tag or args.workload}_{world}")
-    if rank == 0:
+    if rank == 0 and not os.path.isdir(path):
         n = len(cells)
         idx = np.arange(rows) % n
         tbl = pa.table({"image": pa.array([cells[i] for i in idx], pa.binary()),
@@ -648,7 +682,8 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     # 3 in flight as the resident leg: the configs' batches of 128 need the
     # concurrency more than the copy stream (DMA on the slot streams here,
     # DecodePipeline's choice at depth 3)
-    fn = ldt_amd.make_to_tensor_fn(depth=args.dataset_depth or None, device=dev, register=not args.dataset_copy)
+    fn = ldt_amd.make_to_tensor_fn(depth=None if copy else (args.dataset_depth or None), device=dev,
+                                   register=not copy)
     fn.pipeline.set_option(_lib.OPT_RESIZE_IMPL, args.resize_impl)
     ds = ldt_amd.LanceDataset(path, batch_size=B, sampler=sampler, to_tensor_fn=fn)
 
@@ -675,7 +710,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
         dist.all_reduce(tt)
         tot_imgs = int(tt.item())
     barrier()
-    if rank == 0:
+    if rank == 0 and not keep:
         shutil.rmtree(path, ignore_errors=True)
     info = {"sampler": type(sampler).__name__ + ("(pad=True)" if wl["sampler"] == "fragment" else ""),
             "rows": rows, "fragments": sizes if len(sizes) <= 16 else f"{len(sizes)} fragments",
@@ -684,11 +719,128 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
             "timing": "full epochs per rank (plan + every batch, padding included) between barriers, "
                       "max over ranks",
             "harness": (f"LanceDataset(path, batch_size, sampler, to_tensor_fn=make_to_tensor_fn(depth={fn.pipeline.depth}, "
-                        f"register={not args.dataset_copy}))")}
+                        f"register={not copy}))")}
     return tot_imgs / t, info
 
 
-PROFILE_ROUND = "r4"  # committed PMC summaries: this round's, else the newest earlier one
+def _warm_then_time(step, steps, warm, min_s, barrier, max_over_ranks):
+    """At least `warm` untimed steps and `min_s` seconds, then exactly `steps`
+    timed between barriers (max over ranks)."""
+    t_w = time.perf_counter()
+    n = 0
+    while n < warm or time.perf_counter() - t_w < min_s:
+        step()
+        n += 1
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier()
+    return max_over_ranks(time.perf_counter() - t0)
+
+
+def leg_c5(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
+    """BASELINE configs[4]: raw uint8 HWC 1024x1024 -> Resize(224,224) +
+    Normalize (lance_iterable.py:29-31), batch 1024 per GPU, the HBM-roofline
+    stress of the resize/normalise stage. `value`: the cells in HBM (generated
+    there); roofline from the resize launches' HIP events over the timed
+    region; `value_host_input` (N=1): the same batch from pageable host memory
+    through ldt_resize_raw (pinned copy + one H2D per step: PCIe/host bound,
+    SURVEY.md §8(d)); CPU leg: Pillow resize + to_tensor + Normalize."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib
+
+    B, H, W = WORKLOADS["c5"]["batch"], 1024, 1024
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    raw = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
+    ctx = _lib.get_context(dev.index)
+    ctx.set_option(_lib.OPT_PROFILE, 1)
+    K = max(args.steps, 20)
+    ctx.stage_times(reset=True)
+    t = _warm_then_time(lambda: ldt_amd.resize_raw(raw, H, W, normalize=True), K, 3, 0.25, barrier, max_over_ranks)
+    st = ctx.stage_times(reset=True)
+    bpi = H * W * 3 + OUT_BYTES
+    ms, n = st["resize"]
+    avg_s = ms / max(n, 1) / 1e3
+    ach = bpi * B / avg_s / 1e9 if avg_s > 0 else 0.0
+    leg = {"workload": f"c5: {WORKLOADS['c5']['desc']}", "per_gpu_batch": B,
+           "value": round(B * K * world / t, 1), "value_per_gpu": round(B * K / t, 1),
+           "input": "resident (generated in HBM)", "steps": K, "ms_per_step": round(t / K * 1e3, 3),
+           "roofline": {"kernel": "k_resize4<raw> (BILINEAR 224 + Normalize store)", "bound": "hbm",
+                        "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_unit": bpi,
+                        "unit_basis": "SURVEY.md §8(d): 1024*1024*3 + 602,112 B per image",
+                        "avg_launch_ms": round(avg_s * 1e3, 4),
+                        "timing": "HIP events around every resize launch over the timed region (one batch in "
+                                  "flight, so per-launch durations)"}}
+    tr = load_profile("traffic_c5.json")
+    if tr is not None and tr.get("batch", B) == B:
+        leg["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+        leg["roofline"]["traffic_source"] = tr.get("source")
+    if world == 1:
+        host = raw.cpu()
+        th = _warm_then_time(lambda: ldt_amd.resize_raw(host, H, W, normalize=True), 3, 1, 0.0, barrier,
+                             max_over_ranks)
+        leg["value_host_input"] = round(B * 3 / th, 1)
+        leg["value_host_input_note"] = ("pageable host uint8 [1024,1024,1024,3] -> ldt_resize_raw: pinned "
+                                        "copy + one 3.2 GB H2D per step, then the kernel (3 timed steps); "
+                                        "bound by the host copy and PCIe, not the GPU")
+        del host
+    if cpu_ok:
+        leg["cpu_baseline"] = cpu_baseline_raw(raw[:8].cpu().numpy(), budget_s=3.0)
+        leg["gpu_over_cpu"] = round(leg["value"] / leg["cpu_baseline"]["value"], 1)
+    del raw
+    torch.cuda.empty_cache()
+    return leg
+
+
+def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
+    """The c2 images encoded progressive (SOF2), batch
+    256, 7 in flight (DecodePipeline: 4 slots on high-priority streams):
+    `value` with the cells resident, `value_host_input` through
+    make_to_tensor_fn(depth=7) from a host RecordBatch; CPU leg: the
+    reference map-style DataLoader at this box's CPU share of workers."""
+    import numpy as np
+    import pyarrow as pa
+    import torch
+
+    import ldt_amd
+
+    B = WORKLOADS["c2p"]["batch"]
+    cells, labels = make_cells("c2p", B, seed=1000 * rank)
+    rb = ldt_amd.ResidentBatch(cells, labels, device=dev)
+    pipe = ldt_amd.DecodePipeline(depth=7, device=dev, profile=True)
+    K = max(args.steps, 20)
+    pipe.stage_times(reset=True)
+    t = _warm_then_time(lambda: pipe.decode(rb), K, 15, 0.25, barrier, max_over_ranks)
+    st = pipe.stage_times(reset=True)
+    pipe.check()
+    leg = {"workload": f"c2p: {WORKLOADS['c2p']['desc']}", "per_gpu_batch": B, "pipeline_depth": 7,
+           "value": round(B * K * world / t, 1), "value_per_gpu": round(B * K / t, 1), "steps": K,
+           "compressed_bytes_per_img": round(float(np.mean([len(c) for c in cells])), 1),
+           "stages_ms_per_launch": {k: round(v[0] / max(v[1], 1), 4) for k, v in st.items()}}
+    del pipe
+    host = pa.RecordBatch.from_arrays([pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
+                                      names=["image", "label"])
+    fn = ldt_amd.make_to_tensor_fn(depth=7, device=dev)
+    th = _warm_then_time(lambda: fn(host), K, 15, 0.25, barrier, max_over_ranks)
+    fn.check()
+    leg["value_host_input"] = round(B * K * world / th, 1)
+    leg["value_host_input_per_gpu"] = round(B * K / th, 1)
+    del fn
+    torch.cuda.synchronize(dev)
+    if cpu_ok:
+        share = min(len(os.sched_getaffinity(0)), CPU_SHARE)
+        cb = cpu_baseline(cells, labels, reps=3, workers=[share])
+        leg["cpu_baseline"] = cb
+        leg["gpu_over_cpu_host_input"] = round(leg["value_host_input"] / cb["value"], 1)
+    return leg
+
+
+PROFILE_ROUND = "r5"  # committed PMC summaries: this round's, else the newest earlier one
 
 
 def stream_copy_ceiling(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
@@ -740,7 +892,7 @@ def ldt_amd_dims(cell: bytes):
     raise ValueError("no SOF")
 
 
-def cpu_baseline_raw(hwc):
+def cpu_baseline_raw(hwc, budget_s: float = 5.0):
     """Config 5 CPU leg: Pillow resize + to_tensor + Normalize, 1 process."""
     import numpy as np
     from PIL import Image
@@ -749,7 +901,7 @@ def cpu_baseline_raw(hwc):
     STD = np.asarray((0.229, 0.224, 0.225), np.float32)[:, None, None]
     t0 = time.perf_counter()
     reps = 0
-    while time.perf_counter() - t0 < 5.0:
+    while time.perf_counter() - t0 < budget_s:
         for k in range(len(hwc)):
             rs = np.asarray(Image.fromarray(hwc[k]).resize((224, 224), Image.BILINEAR))
             t = rs.transpose(2, 0, 1).astype(np.float32) / np.float32(255)

@@ -407,7 +407,9 @@ __device__ __forceinline__ int write_run(Rd<W> &R, St &st, const Dec &dec, int32
   bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   int iters = 0;
   while (go) {
+#ifndef LDT_NO_WRITE_COUNT
     ++iters;
+#endif
     R.refill();
     const bool first = st.k == 0; // a block starts: its DC symbol
     const uint32_t pk = R.peek();

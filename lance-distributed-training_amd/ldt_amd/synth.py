@@ -32,6 +32,19 @@ def field(h: int, w: int, seed: int, noise: float = 20.0) -> np.ndarray:
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
+def _pmap(fn, n: int) -> list:
+    """[fn(0), ..., fn(n-1)] on a thread pool (Pillow's encoder and numpy's
+    large-array kernels release the GIL); each item is seeded by its index, so
+    the result does not depend on the threads."""
+    if n < 16:
+        return [fn(i) for i in range(n)]
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max(1, min(8, os.cpu_count() or 1))) as ex:
+        return list(ex.map(fn, range(n)))
+
+
 def encode(img: np.ndarray, **save_kwargs) -> bytes:
     from PIL import Image
 
@@ -42,30 +55,28 @@ def encode(img: np.ndarray, **save_kwargs) -> bytes:
 
 def food101_like(n: int, seed: int = 0, noise: float = 6.0) -> Tuple[List[bytes], np.ndarray]:
     """Config 1/3: FOOD101-shaped, PIL defaults (q75 4:2:0, no DRI)."""
-    cells = []
-    for i in range(n):
+    def one(i):
         h, w = FOOD101_SHAPES[(seed + i) % 3]
-        cells.append(encode(field(h, w, seed * 100003 + i, noise)))
-    return cells, np.arange(n, dtype=np.int64) % 101
+        return encode(field(h, w, seed * 100003 + i, noise))
+
+    return _pmap(one, n), np.arange(n, dtype=np.int64) % 101
 
 
 def q90_512(n: int, seed: int = 0, noise: float = 6.0,
             progressive: bool = False) -> Tuple[List[bytes], np.ndarray]:
     """Config 2: 512x512 baseline, 4:2:0, quality 90, no DRI (progressive=True:
     the same images as SOF2, libjpeg's default progression script)."""
-    cells = [encode(field(512, 512, seed * 100003 + i, noise), quality=90, subsampling="4:2:0",
-                    progressive=progressive)
-             for i in range(n)]
+    cells = _pmap(lambda i: encode(field(512, 512, seed * 100003 + i, noise), quality=90, subsampling="4:2:0",
+                                   progressive=progressive), n)
     return cells, np.arange(n, dtype=np.int64) % 101
 
 
 def imagenet_like(n: int, seed: int = 0, noise: float = 6.0) -> Tuple[List[bytes], np.ndarray]:
     """Config 4: variable ~500x375 (W in [333,500], H in [250,500]), q90, restart every MCU row."""
     r = np.random.RandomState(seed + 7)
-    cells = []
-    for i in range(n):
-        w, h = int(r.randint(333, 501)), int(r.randint(250, 501))
-        cells.append(encode(field(h, w, seed * 100003 + i, noise), quality=90, restart_marker_rows=1))
+    dims = [(int(r.randint(333, 501)), int(r.randint(250, 501))) for _ in range(n)]
+    cells = _pmap(lambda i: encode(field(dims[i][1], dims[i][0], seed * 100003 + i, noise), quality=90,
+                                   restart_marker_rows=1), n)
     return cells, np.arange(n, dtype=np.int64) % 1000
 
 

@@ -12,10 +12,19 @@ from ldt_amd import _lib, synth  # noqa: E402
 ctx = _lib.get_context(0)
 names = ["redo", "wgs", "rounds_sum", "rounds_max", "memo_hits", "write_syms", "write_wave_max", "fallbacks",
          "t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "need_lanes", "need_waves", "t_dc_idct"]
+want = sys.argv[1:] or ["c2", "c1", "c4"]
+ctx.set_option(_lib.OPT_PROFILE, 1)
 for wl, fn, n in (("c2", synth.q90_512, 256), ("c1", synth.food101_like, 128), ("c4", synth.imagenet_like, 128)):
+    if wl not in want:
+        continue
     cells, labels = fn(n, seed=1000)
     rb = ldt_amd.ResidentBatch(cells, labels)
     rb.decode()
+    # standalone stage times (one batch in flight): 4 batches after a warm one
+    ctx.stage_times(reset=True)
+    for _ in range(4):
+        rb.decode()
+    st = {k: round(v[0] / max(v[1], 1), 4) for k, v in ctx.stage_times(reset=True).items()}
     out = np.zeros(16, np.int32)
     ctx.check(ctx.lib.ldt_debug_counters(ctx.handle, out.ctypes.data, None), "dbg")
     d = dict(zip(names, out[:16].tolist()))
@@ -29,4 +38,5 @@ for wl, fn, n in (("c2", synth.q90_512, 256), ("c1", synth.food101_like, 128), (
     d["write_syms_per_img"] = round(d["write_syms"] / w, 1)
     d["write_syms_per_lane"] = round(d["write_syms"] / w / 1024, 2)
     d["write_wave_max_per_lane"] = round(d["write_wave_max"] / w / 16, 2)
+    d["stage_ms"] = st
     print(wl, d, flush=True)
