@@ -438,7 +438,15 @@ def main():
     # the rank's GPU-local NUMA node)
     host_ranks = None
     if host_info is not None:
-        mine = {"rank": rank, "local_rank": local, "device": dev.index, "host_us_per_call": host_us,
+        # the rank's host traffic (DESIGN.md §6 host budget): cells moved to
+        # HBM per second by the copying leg (= its H2D rate), the copy pool's
+        # DRAM rate while it copies (bytes per call / its span), and this
+        # box's pinned H2D ceiling
+        cell_bytes = comp_bytes * B
+        host_gbs = {"h2d_gbs": round(cell_bytes * value_host / world / B / 1e9, 2),
+                    "copy_pool_gbs": round(cell_bytes / max(host_us.get("copy_span", 0.0), 1e-3) / 1e3, 2),
+                    "h2d_ceiling_gbs": round(h2d_ceiling(dev), 2)}
+        mine = {"rank": rank, "local_rank": local, "device": dev.index, "host_us_per_call": host_us, **host_gbs,
                 **{k_: host_info[k_] for k_ in ("copy_threads", "copy_cpus", "gpu_numa", "quota_cpus",
                                                  "local_world")}}
         if world > 1:
@@ -841,6 +849,27 @@ def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
 
 
 PROFILE_ROUND = "r5"  # committed PMC summaries: this round's, else the newest earlier one
+
+
+def h2d_ceiling(dev, nbytes: int = 256 << 20, reps: int = 5) -> float:
+    """Pinned host -> HBM copy rate in GB/s (best of `reps` 256 MB DMAs)."""
+    import torch
+
+    src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    best = 0.0
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src, non_blocking=True)
+        e1.record()
+        e1.synchronize()
+        best = max(best, nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9)
+    del src, dst
+    return best
 
 
 def stream_copy_ceiling(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:

@@ -87,6 +87,10 @@ extern "C" {
                                  wave of resize waves on the device (10..1000,
                                  default 100); more bands fill the pipeline's
                                  CU gaps, fewer keep the kernel efficient      */
+#define LDT_OPT_DEBUG_COUNTERS 16 /* 1: the decoders count their phases (cycle
+                                 stamps, rounds, symbols) into the plan blob,
+                                 read with ldt_debug_counters; 0 (default): no
+                                 counters (their atomics cost kernel time)     */
 #define LDT_OPT_RESIZE_WG_WAVES 15 /* waves (one band each) per k_resize4
                                  workgroup for JPEG sources: 0 default (2),
                                  1, 2 or 4; a 1-wave workgroup (~14 KB of LDS

@@ -90,6 +90,7 @@ struct ldt_ctx {
   bool copy_nt = true;    // LDT_OPT_COPY_NT: non-temporal stores into the slot
   int copy_mode = 0;      // LDT_OPT_COPY_MODE: 0 DMA on the device's copy stream, 1 on the caller's
   bool host_timing = false;
+  bool debug_counters = false; // LDT_OPT_DEBUG_COUNTERS
   CopyPlacement placement; // of the current pool
   static constexpr int kSlots = 2;
   // device cells, one buffer per pinned slot: a copy-stream DMA into one may
@@ -969,14 +970,15 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.n_chunks = n_chunks;
   p.n_ds_img = n_ds_img;
   p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
-  p.redo = reinterpret_cast<int32_t *>(dp + off_redo);
+  // diagnostic counters only on request: their atomics cost the kernels time
+  p.redo = c->debug_counters ? reinterpret_cast<int32_t *>(dp + off_redo) : nullptr;
   p.max_tabs = max_tabs;
   p.n_fast420 = n_fast420;
   p.n_prog = (int)prog_img.size();
   p.prog_img = reinterpret_cast<const int32_t *>(dp + off_pimg);
   p.pscans = reinterpret_cast<const ProgScan *>(dp + off_pscan);
   p.ptabs = reinterpret_cast<const ProgTab *>(dp + off_ptab);
-  c->last_off_redo = off_redo;
+  c->last_off_redo = c->debug_counters ? off_redo : -1;
   c->last_plan_dev = dp;
   DevWork w;
   w.data = dev_cells;
@@ -1186,6 +1188,9 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
   case LDT_OPT_SYNC_WARM:
     if (value < 0 || value > 200) return set_err(c, LDT_ERR_ARG, "sync warm-up %lld", (long long)value);
     c->warm_pct = (int)value;
+    return LDT_OK;
+  case LDT_OPT_DEBUG_COUNTERS:
+    c->debug_counters = value != 0;
     return LDT_OK;
   case LDT_OPT_RESIZE_IMPL:
     if (value < 0 || value > 2) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);
@@ -1482,7 +1487,8 @@ int ldt_distributed_indices(ldt_ctx *c, int64_t dataset_len, int num_replicas, i
 int ldt_debug_counters(ldt_ctx *c, int32_t *out16, void *stream) {
   if (!c || !out16) return LDT_ERR_ARG;
   DeviceGuard g(c->device);
-  if (c->last_off_redo < 0) return set_err(c, LDT_ERR_ARG, "no batch yet");
+  if (c->last_off_redo < 0)
+    return set_err(c, LDT_ERR_ARG, "no batch decoded with LDT_OPT_DEBUG_COUNTERS = 1 yet");
   HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
   HIPCHK(c, hipMemcpy(out16, c->last_plan_dev + c->last_off_redo, 64,
                       hipMemcpyDeviceToHost));

@@ -407,9 +407,7 @@ __device__ __forceinline__ int write_run(Rd<W> &R, St &st, const Dec &dec, int32
   bool go = (R.p < stop || st.k != 0) && !(st.k == 0 && cursor + 1 >= lim);
   int iters = 0;
   while (go) {
-#ifndef LDT_NO_WRITE_COUNT
     ++iters;
-#endif
     R.refill();
     const bool first = st.k == 0; // a block starts: its DC symbol
     const uint32_t pk = R.peek();
@@ -771,6 +769,7 @@ struct ImgLds {
   // writes)
   alignas(16) int32_t ds_endw[kHuffThreads / 64];
   int32_t need_lanes, need_waves, memo_hits; // diagnostic counters (summed over rounds)
+  int32_t w_syms, w_wmax;                      // ... and of the write pass
 };
 static_assert(sizeof(ImgLds) + 512 <= kHuffStaticLds, "k_huff_image static LDS");
 static_assert(sizeof(ImgLds) >= 4 * (kHuffThreads / 64) * sizeof(int32_t), "dc_scan_image scratch");
@@ -893,7 +892,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   for (int round = 0; round <= kHuffThreads; ++round) {
     ++rounds;
     __syncthreads(); // states published
-    if (round == 0 && tid == 0) t_ph1 = wall_clock64();
+    if (dbg && round == 0 && tid == 0) t_ph1 = wall_clock64();
     // A slot whose predecessor's exit equals the entry of its previous
     // trajectory adopts that trajectory again (exits flip between two values
     // while an unsynchronised stretch converges); repeated until no slot
@@ -999,7 +998,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     __syncthreads();
     if (!sh.any_changed) break;
   }
-  const uint64_t t_rounds = wall_clock64();
+  const uint64_t t_rounds = dbg ? wall_clock64() : 0;
   if (dbg && tid == 0) {
     atomicAdd(dbg + 1, 1);
     atomicAdd(dbg + 2, rounds);
@@ -1021,7 +1020,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   const int pre = block_excl_scan1024(live ? (int)sh.nblk[tid] : 0, sh.scan, &tot);
   sh.ex_p[tid] = pre;
   __syncthreads();
-  const uint64_t t_scan = wall_clock64();
+  const uint64_t t_scan = dbg ? wall_clock64() : 0;
 
   // ---- write pass from the true entry ----
   // block records into LDS (the slot state is dead from here) when they fit
@@ -1057,7 +1056,12 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   // agent-scope fence would write back and invalidate the XCD's whole L2.
   trunc = __syncthreads_or(trunc);
   if (dbg) {
-    // write-pass symbols: summed over the lanes, and the waves' slowest lanes
+    // diagnostics (LDT_OPT_DEBUG_COUNTERS): phase times in 10 ns ticks and
+    // write-pass symbols (summed over the lanes, and the waves' slowest
+    // lanes), summed over images; per wave into LDS, one global atomic per
+    // counter and workgroup (same-address atomics of every wave cost the
+    // kernel ~20% when they were global)
+    const uint64_t t_end = wall_clock64();
     int wsum = witers, wmax = witers;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1065,20 +1069,21 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
       wmax = max(wmax, __shfl_xor(wmax, o));
     }
     if ((tid & 63) == 0) {
-      atomicAdd(dbg + 5, wsum);
-      atomicAdd(dbg + 6, wmax);
+      atomicAdd(&sh.w_syms, wsum);
+      atomicAdd(&sh.w_wmax, wmax);
     }
-  }
-  // diagnostic phase times (10 ns ticks summed over images; ldt_debug_counters)
-  if (dbg && tid == 0) {
-    const uint64_t t_end = wall_clock64();
-    atomicAdd(dbg + 9, (int)(t_ph1 - t_setup));
-    atomicAdd(dbg + 10, (int)(t_rounds - t_ph1));
-    atomicAdd(dbg + 11, (int)(t_scan - t_rounds));
-    atomicAdd(dbg + 12, (int)(t_end - t_scan));
-    atomicAdd(dbg + 13, sh.need_lanes);
-    atomicAdd(dbg + 14, sh.need_waves);
-    atomicAdd(dbg + 4, sh.memo_hits);
+    __syncthreads();
+    if (tid == 0) {
+      atomicAdd(dbg + 5, sh.w_syms);
+      atomicAdd(dbg + 6, sh.w_wmax);
+      atomicAdd(dbg + 9, (int)(t_ph1 - t_setup));
+      atomicAdd(dbg + 10, (int)(t_rounds - t_ph1));
+      atomicAdd(dbg + 11, (int)(t_scan - t_rounds));
+      atomicAdd(dbg + 12, (int)(t_end - t_scan));
+      atomicAdd(dbg + 13, sh.need_lanes);
+      atomicAdd(dbg + 14, sh.need_waves);
+      atomicAdd(dbg + 4, sh.memo_hits);
+    }
   }
   if (trunc) return; // a failed image's records are never read
   // ---- DC predictors (the serial path runs k_dc_scan instead), in the
@@ -1259,7 +1264,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
   const int tid = threadIdx.x;
-  const uint64_t t_start = wall_clock64();
+  const uint64_t t_start = dbg ? wall_clock64() : 0;
   // dynamic LDS: [window win_bytes][tables]
   LDS_AS uint8_t *tabs = (LDS_AS uint8_t *)(dyn_lds + win_bytes / 4);
   SlotTabs slot_tab;
@@ -1279,6 +1284,8 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     sh.need_lanes = 0;
     sh.need_waves = 0;
     sh.memo_hits = 0;
+    sh.w_syms = 0;
+    sh.w_wmax = 0;
   }
   const int64_t need = destuff_region_bytes(d.src_len, d.nseg) + 16;
   const bool in_lds = need <= win_bytes;
@@ -1348,7 +1355,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     }
   }
   __syncthreads();
-  const uint64_t t_setup = wall_clock64();
+  const uint64_t t_setup = dbg ? wall_clock64() : 0;
   if (dbg && tid == 0) atomicAdd(dbg + 8, (int)(t_setup - t_start));
   const int warm = (d.sub_bits * warm_pct) / 100;
   if (in_lds)

@@ -60,6 +60,7 @@ OPT_COPY_MODE = 12
 OPT_COPY_BIND = 13
 OPT_COPY_NT = 14
 OPT_RESIZE_WG_WAVES = 15
+OPT_DEBUG_COUNTERS = 16
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
 HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status", "copy_wake", "copy_span")

@@ -4,6 +4,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "lance-di
 import torch, ldt_amd
 from ldt_amd import _lib, synth
 ctx = _lib.get_context(0)
+ctx.set_option(_lib.OPT_DEBUG_COUNTERS, 1)
 names = ["redo", "wgs", "rounds_sum", "rounds_max", "walks", "walk_first", "walk_steps", "fallbacks", "boundaries"]
 for wl, fn, n in (("c2", synth.q90_512, 64), ("c1", synth.food101_like, 64), ("c4", synth.imagenet_like, 64)):
     cells, labels = fn(n, seed=1)

@@ -12,6 +12,7 @@ from ldt_amd import _lib, synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 ctx = _lib.get_context(0)
+ctx.set_option(_lib.OPT_DEBUG_COUNTERS, 1)
 cells, labels = synth.q90_512(n, seed=0, progressive=True)
 rb = ldt_amd.ResidentBatch(cells, labels)
 for rep in range(2):
