@@ -137,6 +137,11 @@ ldt_ctx *ldt_create(int device, size_t max_batch_bytes, int max_n);
 void ldt_destroy(ldt_ctx *ctx);
 const char *ldt_last_error(ldt_ctx *ctx);
 int ldt_set_option(ldt_ctx *ctx, int option, int64_t value);
+/* The hipStream_t a host batch's cells go to HBM on under LDT_OPT_COPY_MODE 0
+ * (NULL, the default: a per-device copy stream the library creates). The
+ * stream must outlive the context's use of it; the decode stream waits for
+ * the DMA with an event, and the DMA waits for the slot's previous readers. */
+int ldt_set_copy_stream(ldt_ctx *ctx, void *stream);
 /* Library version string, e.g. "ldt 0.1.0 gfx950". */
 const char *ldt_version(void);
 

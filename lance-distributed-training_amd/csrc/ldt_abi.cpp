@@ -89,6 +89,7 @@ struct ldt_ctx {
   int copy_bind = 2;      // LDT_OPT_COPY_BIND: pool threads on GPU-local cores' L3 domains (1: the cores)
   bool copy_nt = true;    // LDT_OPT_COPY_NT: non-temporal stores into the slot
   int copy_mode = 0;      // LDT_OPT_COPY_MODE: 0 DMA on the device's copy stream, 1 on the caller's
+  hipStream_t copy_stream = nullptr; // ldt_set_copy_stream: replaces the device's copy stream (mode 0)
   bool host_timing = false;
   bool debug_counters = false; // LDT_OPT_DEBUG_COUNTERS
   CopyPlacement placement; // of the current pool
@@ -401,7 +402,7 @@ void build_lut(const ldt_norm *norm, float *lut) {
 // kernels that last read that buffer; `s` waits for it. Mode 1 (or no copy
 // stream): on `s` itself, behind the previous batch's kernels.
 int enqueue_cells(ldt_ctx *c, int sl, const void *src, size_t n, hipStream_t s) {
-  hipStream_t cs = c->copy_mode == 0 ? copy_stream(c->device) : nullptr;
+  hipStream_t cs = c->copy_mode != 0 ? nullptr : (c->copy_stream ? c->copy_stream : copy_stream(c->device));
   if (!cs) {
     HIPCHK(c, hipMemcpyAsync(c->d_data[sl].p, src, n, hipMemcpyHostToDevice, s));
     return LDT_OK;
@@ -1169,6 +1170,16 @@ int ldt_unregister_host(ldt_ctx *c, const void *ptr) {
     HIPCHK(c, hipDeviceSynchronize());
   }
   HIPCHK(c, hipHostUnregister(const_cast<void *>(ptr)));
+  return LDT_OK;
+}
+
+// The stream a context's cells go to HBM on in LDT_OPT_COPY_MODE 0 (NULL:
+// the device's own copy stream). A caller that owns its streams lends one
+// here, so that the DMAs do not add a fifth stream to the process's four
+// hardware queues (DecodePipeline's adaptive mode, transforms.py).
+int ldt_set_copy_stream(ldt_ctx *c, void *stream) {
+  if (!c) return LDT_ERR_ARG;
+  c->copy_stream = (hipStream_t)stream;
   return LDT_OK;
 }
 

@@ -251,7 +251,10 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   // kernel is LDS-bound). JPEG rows stay plain: the skew's extra registers
   // cost a wave per SIMD there, which is worth more than its 2-way conflicts.
   constexpr bool kJpeg = SRC == 0 || SRC == 2 || SRC == 5;
-  constexpr bool kSkew = !kJpeg;
+#ifndef LDT_RESIZE_SKEW420
+#define LDT_RESIZE_SKEW420 0
+#endif
+  constexpr bool kSkew = !kJpeg || (SRC == 5 && LDT_RESIZE_SKEW420);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
   for (int i = tid; i < 768; i += (int)blockDim.x) s_lut[i] = lut[i];
@@ -430,7 +433,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
             px[j] = __builtin_amdgcn_perm(xb, __builtin_amdgcn_perm(xg, xr, 0x0C0C0602u), 0x0C060100u);
           }
           if (x0 < W) {
-            uint4 *dq = reinterpret_cast<uint4 *>((r ? s1 : s0) + x0);
+            uint4 *dq = reinterpret_cast<uint4 *>((r ? s1 : s0) + skw<kSkew>(x0));
             dq[0] = make_uint4(px[0], px[1], px[2], px[3]);
             dq[1] = make_uint4(px[4], px[5], px[6], px[7]);
           }

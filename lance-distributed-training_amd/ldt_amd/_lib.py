@@ -67,7 +67,7 @@ HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status", "copy_w
 
 # Every symbol include/ldt.h declares (checked by tests/test_abi.py).
 EXPORTED = (
-    "ldt_create", "ldt_destroy", "ldt_last_error", "ldt_set_option", "ldt_version",
+    "ldt_create", "ldt_destroy", "ldt_last_error", "ldt_set_option", "ldt_set_copy_stream", "ldt_version",
     "ldt_decode_batch", "ldt_decode_batch_large", "ldt_decode_batch_resident",
     "ldt_register_host", "ldt_unregister_host", "ldt_fetch_status", "ldt_last_ticket", "ldt_fetch_status_ticket",
     "ldt_stage_times", "ldt_host_times", "ldt_host_info", "ldt_resize_raw", "ldt_shard_ranges",
@@ -129,6 +129,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_last_error.argtypes = [vp]
         L.ldt_last_error.restype = ctypes.c_char_p
         L.ldt_set_option.argtypes = [vp, i32, i64]
+        L.ldt_set_copy_stream.argtypes = [vp, vp]
         L.ldt_version.argtypes = []
         L.ldt_version.restype = ctypes.c_char_p
         L.ldt_decode_batch.argtypes = [vp, vp, vp, i64, i64, vp, vp, i64, vp, vp, vp, vp, vp]
@@ -150,7 +151,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         L.ldt_debug_counters.argtypes = [vp, vp, vp]
         L.ldt_register_host.argtypes = [vp, vp, sz]
         L.ldt_unregister_host.argtypes = [vp, vp]
-        for name in ("ldt_set_option", "ldt_decode_batch", "ldt_decode_batch_large", "ldt_register_host",
+        for name in ("ldt_set_option", "ldt_set_copy_stream", "ldt_decode_batch", "ldt_decode_batch_large", "ldt_register_host",
                      "ldt_unregister_host",
                      "ldt_decode_batch_resident", "ldt_fetch_status", "ldt_fetch_status_ticket", "ldt_resize_raw", "ldt_stage_times", "ldt_host_times", "ldt_host_info",
                      "ldt_shard_ranges", "ldt_shard_fragments", "ldt_distributed_indices",
@@ -180,6 +181,12 @@ class Context:
 
     def set_option(self, opt: int, value: int) -> None:
         self.check(self.lib.ldt_set_option(self.handle, opt, int(value)), "ldt_set_option")
+
+    def set_copy_stream(self, stream) -> None:
+        """The stream (a torch.cuda.Stream, or None for the library's own)
+        this context's host cells go to HBM on under LDT_OPT_COPY_MODE 0."""
+        self.check(self.lib.ldt_set_copy_stream(self.handle, stream.cuda_stream if stream is not None else None),
+                   "ldt_set_copy_stream")
 
     def stage_times(self, reset: bool = False):
         """{stage: (total_ms, launches)} from LDT_OPT_PROFILE events."""

@@ -576,6 +576,16 @@ class DecodePipeline:
     previous one — the GPU-side analogue of the reference DataLoader's
     prefetching workers (lance_map_style.py:137, num_workers=8).
 
+    ``adaptive=True`` (``depth`` 3, what ``make_to_tensor_fn()`` builds):
+    the batches in flight follow each call's batch size, with the process's
+    four hardware queues held by the consumer's stream and the three slot
+    streams throughout. A host batch of at least 8 MB of encoded cells takes
+    slots 0 and 1 in turn with its DMA on slot 2's stream (two in flight, the
+    transfer overlapping the previous batches' kernels); smaller batches and
+    resident ones rotate over all three slots with the DMA on the slot's own
+    stream (three in flight: a batch of 128 small images does not fill the
+    GPU). DESIGN.md §7a.
+
     Errors are asynchronous: every decode gets its context's ticket
     (ldt_last_ticket), and ``check()`` waits for every unchecked batch and
     raises ImageDecodeError with its failing rows (per-image status, as
@@ -584,11 +594,12 @@ class DecodePipeline:
     long finished — so checking before each reuse never waits for the batch
     just enqueued."""
 
-    def __init__(self, depth: int = 2, device=None, profile: bool = False):
+    def __init__(self, depth: int = 2, device=None, profile: bool = False, adaptive: bool = False):
         from collections import deque
 
         self.dec = _decoder(device)
-        self.depth = max(1, int(depth))
+        self.depth = 3 if adaptive else max(1, int(depth))
+        self.adaptive = bool(adaptive)
         self.ctxs = [_lib.Context(self.dec.device.index) for _ in range(self.depth)]
         for c in self.ctxs:
             c.set_option(_lib.OPT_SYNC_STATUS, 0)
@@ -607,12 +618,20 @@ class DecodePipeline:
         # c2p depth 4: 26k img/s on normal streams vs 44k). LDT_SLOT_PRIORITY
         # = 0 / 1 forces either.
         n_high, slot_dma = slot_streams(self.depth, _lib.hw_queues(), os.environ.get("LDT_SLOT_PRIORITY"))
+        if self.adaptive:
+            n_high, slot_dma = 0, True
         self.high_priority = n_high > 0
         if slot_dma:
             for c in self.ctxs:
                 c.set_option(_lib.OPT_COPY_MODE, 1)
         self.streams = [torch.cuda.Stream(self.dec.device, priority=-1 if i < n_high else 0)
                         for i in range(self.depth)]
+        # adaptive: slots 0 and 1 DMA large batches on slot 2's stream
+        self._copy_mode = [1 if slot_dma else 0] * self.depth
+        self._k_large = self._k_small = 0
+        if self.adaptive:
+            for c in self.ctxs[:2]:
+                c.set_copy_stream(self.streams[2])
         self.pending = [deque() for _ in range(self.depth)]  # per slot: (ticket, n), oldest first
         self.last_ticket = None  # (slot, ticket) of the most recent decode
         self.k = 0
@@ -629,7 +648,21 @@ class DecodePipeline:
         ``(image, label, ready)`` and the consumer calls ``ready()`` on the
         stream that will use the tensors, so work enqueued there in between
         (a training step) overlaps this decode (see ``prefetch``)."""
-        slot = self.k % self.depth
+        if self.adaptive:
+            large = not isinstance(batch, ResidentBatch) and \
+                auto_host_depth(_cell_bytes(batch, image_column)) == 2
+            if large:
+                slot = self._k_large % 2
+                self._k_large += 1
+            else:
+                slot = self._k_small % 3
+                self._k_small += 1
+            mode = 0 if large else 1
+            if self._copy_mode[slot] != mode:
+                self.ctxs[slot].set_option(_lib.OPT_COPY_MODE, mode)
+                self._copy_mode[slot] = mode
+        else:
+            slot = self.k % self.depth
         # the slot's context holds the status of its last two calls: check the
         # older one before this call replaces it (it finished long ago)
         self.check_slot(slot)
@@ -700,7 +733,6 @@ class DecodePipeline:
             return _as_device_batch(img, lbl)
 
         for b in batches:
-            self.check_slot(self.k % self.depth)
             q.append(self.decode(b, normalize=normalize, image_column=image_column,
                                  label_column=label_column, wait=False) + (self.last_ticket,))
             if len(q) > ahead:
@@ -785,8 +817,10 @@ AUTO_DEPTH_SMALL_BYTES = 8 << 20
 
 
 def auto_host_depth(cell_bytes: int) -> int:
-    """Batches in flight that make_to_tensor_fn(depth=None) picks for a batch
-    of `cell_bytes` bytes of encoded cells."""
+    """Batches in flight that make_to_tensor_fn(depth=None) (an adaptive
+    DecodePipeline) runs a host batch of `cell_bytes` bytes of encoded cells
+    at: 2 (its DMA on a stream of its own) from AUTO_DEPTH_SMALL_BYTES on, 3
+    below."""
     return 3 if 0 < cell_bytes < AUTO_DEPTH_SMALL_BYTES else 2
 
 
@@ -818,23 +852,19 @@ def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, 
     """A pipelined ``to_tensor_fn`` for ``LanceDataset(..., to_tensor_fn=...)``
     (lance_iterable.py:53-59): each call enqueues its RecordBatch on one of
     `depth` contexts/streams and returns at once, so batch k+1's host copy and
-    kernels overlap batch k's. Depth 2 leaves the cells' copy stream its own
-    hardware queue (DecodePipeline): measured faster on large host batches
-    than depth 3 with the DMA on the slot streams, which small batches prefer
-    (DESIGN.md §7a); the default (None) picks one of the two per function. The tensors are ready on torch's current stream
+    kernels overlap batch k's. The tensors are ready on torch's current stream
     (it waits for the slot's stream). Per-image errors are reported
     asynchronously: by ``fn.check()``, and at the latest when the slot is
     reused a second time (2 * `depth` calls later, when that batch finished
     long ago, so the check never stalls the host) — unlike the synchronous
     ``decode_tensor_image``.
 
-    ``depth=None``: chosen at the first call from its batch, 3 for batches of
-    fewer than 8 MB of encoded cells (FOOD101-shaped batches of 128), else 2
-    (``auto_host_depth``); options set through ``fn.pipeline.set_option``
-    before that call carry over (options set on one of its contexts,
-    ``fn.pipeline.ctxs[i]``, do not: the first call may replace the pipeline). The ``fn.iterate`` (prefetch) path keeps depth 2. A
-    ``LanceDataset`` loop over registered (mapped) fragments should ask for
-    ``depth=3``.
+    ``depth=None`` (the default): the batches in flight follow each call's
+    batch (``DecodePipeline(adaptive=True)``): 2 with the DMA on a stream of
+    its own for batches of at least 8 MB of encoded cells (c2-shaped batches
+    of 256), 3 with the DMA on the slot's stream below that (FOOD101-shaped
+    batches of 128), ``auto_host_depth``. With
+    ``register=True`` it means 3 (registered sources: DESIGN.md §8).
 
     ``prefetch=k`` (k < depth): ``LanceDataset`` iterates through
     ``fn.iterate`` instead, enqueueing the next k batches before yielding each
@@ -851,31 +881,20 @@ def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, 
     raising (ldt.h: such a range stays on the copying path)."""
     from collections import OrderedDict
 
-    auto = depth is None
     # (registered sources have no size-independent best depth: LanceDataset
     # over registered c2 fragments 436-475k img/s at depth 3 vs 297-308k at 2,
     # two alternating registered c2 batches 389k at 3 vs 572-583k at 2;
-    # profiles/r4/dataset_depth_ab_r4dd.txt; a dataset loop asks for depth=3)
-    pipe = DecodePipeline(depth=2 if auto else depth, device=device)
+    # profiles/r4/dataset_depth_ab_r4dd.txt: 3 for them)
+    if depth is None and register:
+        depth = 3
+    pipe = DecodePipeline(depth=depth or 3, device=device, adaptive=depth is None)
     image_column = fixed.get("image_column", "image")
-    # depth=None: the options set on the first pipeline, replayed on the one
-    # the first batch picks
-    opts: list = []
-    if auto:
-        _set = pipe.set_option
-
-        def _recording_set_option(opt, value):
-            opts.append((opt, value))
-            _set(opt, value)
-
-        pipe.set_option = _recording_set_option
     owned: "OrderedDict[int, object]" = OrderedDict()  # registrations made here, LRU order
     reg_on = [bool(register)]
     # churn guard: unregistering synchronises the device, so a loader that hands
     # out fresh buffers every batch (instead of slices of mapped fragments)
-    # must not evict on every call; `evictions` holds the call numbers of the
+    # must not evict on every call; `evictions` holds the batch numbers of the
     # recent evictions
-    calls = [0]
     seen = [0]  # batches offered to maybe_register (to_tensor_fn and the fn.iterate path)
     evictions: list = []
 
@@ -913,18 +932,7 @@ def make_to_tensor_fn(depth: Optional[int] = None, device=None, normalize=None, 
             release()
 
     def to_tensor_fn(batch, **kwargs):
-        nonlocal pipe
-        calls[0] += 1
-        if auto and calls[0] == 1:
-            d = auto_host_depth(_cell_bytes(batch, kwargs.get("image_column", image_column)))
-            if d != pipe.depth:
-                pipe = DecodePipeline(depth=d, device=device)
-                for opt, value in opts:
-                    pipe.set_option(opt, value)
-                to_tensor_fn.pipeline = pipe
-                to_tensor_fn.check = pipe.check
         maybe_register(batch, kwargs.get("image_column", image_column))
-        pipe.check_slot(pipe.k % pipe.depth)
         img, lbl = pipe.decode(batch, normalize=kwargs.get("normalize", normalize),
                                image_column=kwargs.get("image_column", fixed.get("image_column", "image")),
                                label_column=kwargs.get("label_column", fixed.get("label_column", "label")))

@@ -1013,11 +1013,13 @@ def test_packed_420_staging_edge_widths():
         _check(out[0][k], oracle.jpeg_to_tensor(cells[k]), f"w{widths[k]}")
 
 
-def test_make_to_tensor_fn_auto_depth():
-    """make_to_tensor_fn() (depth=None): a FOOD101-shaped first batch (< 8 MB
-    of cells) runs 3 deep, a c2-shaped one 2 deep; options set through
-    fn.pipeline before the first call carry over to the pipeline it picks;
-    every call bit-exact against the synchronous decode."""
+def test_make_to_tensor_fn_adaptive_depth():
+    """make_to_tensor_fn() (depth=None): one adaptive pipeline whose batches
+    in flight follow each call's batch: FOOD101-shaped batches (< 8 MB of
+    cells) rotate over three slots with the DMA on the slot's stream,
+    c2-shaped ones (>= 8 MB) over slots 0 and 1 with the DMA on slot 2's
+    stream. Interleaved small and large batches decode bit-exactly as the
+    synchronous decode; options set through fn.pipeline reach every context."""
     import torch
 
     import ldt_amd
@@ -1025,19 +1027,22 @@ def test_make_to_tensor_fn_auto_depth():
 
     small, ls = synth.food101_like(48, seed=61)
     big, lb = synth.q90_512(130, seed=62)  # ~8.7 MB of cells
-    for cells, labels, want in ((small, ls, 3), (big, lb, 2)):
-        rb = _batch(cells, labels)
-        ref = ldt_amd.decode_tensor_image(rb)["image"].cpu().numpy()
-        fn = ldt_amd.make_to_tensor_fn()
-        fn.pipeline.set_option(_lib.OPT_COPY_BIND, 1)
-        fn.pipeline.set_option(_lib.OPT_COPY_THREADS, 2)
-        outs = [fn(rb) for _ in range(5)]
-        fn.check()
-        torch.cuda.synchronize()
-        assert fn.pipeline.depth == want
-        for o in outs:
-            assert np.array_equal(o["image"].cpu().numpy(), ref)
-        info = fn.pipeline.ctxs[0].host_info()
+    rs, rbig = _batch(small, ls), _batch(big, lb)
+    ref_s = ldt_amd.decode_tensor_image(rs)["image"].cpu().numpy()
+    ref_b = ldt_amd.decode_tensor_image(rbig)["image"].cpu().numpy()
+    fn = ldt_amd.make_to_tensor_fn()
+    assert fn.pipeline.adaptive and fn.pipeline.depth == 3
+    fn.pipeline.set_option(_lib.OPT_COPY_BIND, 1)
+    fn.pipeline.set_option(_lib.OPT_COPY_THREADS, 2)
+    order = [rs, rs, rbig, rs, rbig, rbig, rbig, rs, rs, rs, rbig, rs]
+    outs = [fn(b) for b in order]
+    fn.check()
+    torch.cuda.synchronize()
+    for b, o in zip(order, outs):
+        assert np.array_equal(o["image"].cpu().numpy(), ref_s if b is rs else ref_b)
+    assert fn.pipeline._k_large == 5 and fn.pipeline._k_small == 7
+    for c in fn.pipeline.ctxs:
+        info = c.host_info()
         assert info["copy_bind"] == 1 and info["copy_threads"] == 2
 
 

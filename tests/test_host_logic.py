@@ -215,7 +215,7 @@ def test_auto_host_depth_from_cell_bytes():
 class _FakePipeline:
     """DecodePipeline stand-in for host-logic tests (no GPU): records decodes."""
 
-    def __init__(self, depth=2, device=None, profile=False):
+    def __init__(self, depth=2, device=None, profile=False, adaptive=False):
         self.depth = depth
         self.k = 0
         self.ctxs = []

@@ -1,0 +1,158 @@
+/* Offline model (not product code) of k_huff_image's convergence rounds on
+ * one baseline 4:2:0 JPEG without restart markers: phase 1 from the guess
+ * (b = 0, k = 0) at every range start, then rounds of re-decodes from the
+ * predecessor's exit that stop at the first checkpoint (S/3, 2S/3) where
+ * they merge with the slot's previous trajectory, with the memo of the
+ * previous trajectory (ldt_huffman.hip image_decode). SPEC=1 adds the
+ * speculation studied for round 5: every needy slot's successor is also
+ * decoded from the needy slot's old exit (p, k) under the other block
+ * phases b', and a slot whose new entry matches one adopts that result at
+ * the start of the next round.
+ * Prints rounds and the critical path: the sum over rounds of the longest
+ * decode (symbol steps) of the round.
+ * usage: rounds_sim <file.jpg> <S bits (0: auto)> <spec 0/1> [max spec lanes] */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct { int maxcode[18], valoff[18]; uint8_t vals[256]; } Tab;
+static Tab dc[4], ac[4];
+static int cdc[3], cac[3];
+static uint8_t *bits;
+static long nbytes;
+
+static void derive(Tab *t, const uint8_t *cnt, const uint8_t *v) {
+  int code = 0, k = 0;
+  for (int l = 1; l <= 16; l++) {
+    if (cnt[l - 1]) { t->valoff[l] = k - code; code += cnt[l - 1]; k += cnt[l - 1]; t->maxcode[l] = code - 1; }
+    else t->maxcode[l] = -1;
+    code <<= 1;
+  }
+  memcpy(t->vals, v, k);
+}
+static inline uint32_t peek16(long p) {
+  uint32_t w = 0;
+  for (int i = 0; i < 4; i++) { long b = (p >> 3) + i; w = (w << 8) | (b < nbytes ? bits[b] : 0); }
+  return (w << (p & 7)) >> 16;
+}
+static int decode(const Tab *t, long *p) {
+  uint32_t w = peek16(*p);
+  for (int l = 1; l <= 16; l++) { int c = w >> (16 - l); if (c <= t->maxcode[l]) { *p += l; return t->vals[(t->valoff[l] + c) & 255]; } }
+  *p += 16; return 0;
+}
+static const int bcomp[6] = {0, 0, 0, 0, 1, 2};
+typedef struct { long p; int b, k; } St;
+static void step(St *s) {
+  int c = bcomp[s->b];
+  if (s->k == 0) { int t = decode(&dc[cdc[c]], &s->p); s->p += t; s->k = 1; }
+  else {
+    int rs = decode(&ac[cac[c]], &s->p); int r = rs >> 4, t = rs & 15;
+    if (t) { s->k += r + 1; s->p += t; } else s->k = (r == 15) ? s->k + 16 : 64;
+    if (s->k >= 64) { s->k = 0; s->b = (s->b + 1) % 6; }
+  }
+}
+static int eq(St a, St b) { return a.p == b.p && a.b == b.b && a.k == b.k; }
+
+typedef struct { St en, ex, cp[2]; int ncp; } Traj;
+static long S, nbitsl;
+static int nslot;
+
+/* decode slot j from state e to the first boundary >= its range end; with
+ * prev: stop at the first checkpoint equal to prev's (merge). Returns steps. */
+static int run(int j, St e, const Traj *prev, Traj *out) {
+  long stop = (long)(j + 1) * S; if (stop > nbitsl) stop = nbitsl;
+  long c0 = (long)j * S + S / 3, c1 = (long)j * S + (2 * S) / 3;
+  St s = e; int steps = 0; out->en = e; out->ncp = 0;
+  long lims[2] = {c0, c1};
+  for (int c = 0; c < 2; c++) {
+    while (s.p < lims[c] && s.p < stop) { step(&s); steps++; }
+    if (s.p >= stop) { out->ex = s; return steps; }
+    if (prev && prev->ncp > c && eq(prev->cp[c], s)) { out->cp[c] = s; out->ncp = c + 1; out->ex = prev->ex; return steps; }
+    out->cp[c] = s; out->ncp = c + 1;
+  }
+  while (s.p < stop) { step(&s); steps++; }
+  out->ex = s;
+  return steps;
+}
+
+int main(int argc, char **argv) {
+  FILE *f = fopen(argv[1], "rb"); fseek(f, 0, SEEK_END); long L = ftell(f); fseek(f, 0, SEEK_SET);
+  uint8_t *d = malloc(L); if (fread(d, 1, L, f) != (size_t)L) return 1; fclose(f);
+  long i = 2, scan = 0;
+  while (i < L) {
+    int m = d[i + 1], len = (d[i + 2] << 8) | d[i + 3];
+    if (m == 0xC4) { long s = i + 4, e = i + 2 + len; while (s < e) { int tc = d[s] >> 4, th = d[s] & 15; int n = 0; for (int q = 0; q < 16; q++) n += d[s + 1 + q]; derive(tc ? &ac[th] : &dc[th], d + s + 1, d + s + 17); s += 17 + n; } }
+    if (m == 0xDA) { int ns = d[i + 4]; for (int q = 0; q < ns; q++) { int sel = d[i + 6 + 2 * q]; cdc[q] = sel >> 4; cac[q] = sel & 15; } scan = i + 2 + len; break; }
+    i += 2 + len;
+  }
+  bits = malloc(L); nbytes = 0;
+  for (long q = scan; q < L - 1; q++) { if (d[q] == 0xFF) { if (d[q + 1] == 0) { bits[nbytes++] = 0xFF; q++; continue; } break; } bits[nbytes++] = d[q]; }
+  nbitsl = nbytes * 8;
+  S = atol(argv[2]);
+  const int spec = atoi(argv[3]);
+  const int lanes_cap = argc > 4 ? atoi(argv[4]) : 1024;
+  if (S == 0) { S = 256; while ((nbitsl + S - 1) / S > 1024) S += 64; }
+  nslot = (int)((nbitsl + S - 1) / S);
+  Traj *cur = calloc(nslot, sizeof(Traj)), *memo = calloc(nslot, sizeof(Traj));
+  int *has_memo = calloc(nslot, sizeof(int));
+  /* speculation results: per slot, up to 6 (entry, traj) */
+  Traj *sp = calloc((size_t)nslot * 6, sizeof(Traj)); int *nsp = calloc(nslot, sizeof(int));
+  int ph1 = 0;
+  for (int j = 0; j < nslot; j++) { St e = {(long)j * S, 0, 0}; int st = run(j, e, NULL, &cur[j]); if (st > ph1) ph1 = st; }
+  long same_pk = 0, diff_pk = 0;
+  long crit = 0; int rounds = 0, spec_hits = 0, memo_hits = 0, needy_sum = 0;
+  Traj *nw = calloc(nslot, sizeof(Traj)); int *needy = calloc(nslot, sizeof(int)); int *changed = calloc(nslot, sizeof(int));
+  for (;;) {
+    rounds++;
+    /* adoption loop: memo and speculation hits, until none */
+    for (;;) {
+      int any = 0;
+      for (int j = 1; j < nslot; j++) {
+        St pe = cur[j - 1].ex;
+        if (eq(pe, cur[j].en)) continue;
+        if (has_memo[j] && eq(memo[j].en, pe)) { Traj t = cur[j]; cur[j] = memo[j]; cur[j].ncp = 0; memo[j] = t; memo_hits++; any = 1; continue; }
+        if (spec) for (int a = 0; a < nsp[j]; a++) if (eq(sp[(size_t)j * 6 + a].en, pe)) {
+          memo[j] = cur[j]; has_memo[j] = 1; cur[j] = sp[(size_t)j * 6 + a]; cur[j].ncp = 0; spec_hits++; any = 1; break;
+        }
+      }
+      if (!any) break;
+    }
+    int tot = 0;
+    for (int j = 1; j < nslot; j++) { needy[j] = !eq(cur[j - 1].ex, cur[j].en); tot += needy[j]; }
+    if (!tot) break;
+    needy_sum += tot;
+    int mx = 0, any_changed = 0;
+    for (int j = 1; j < nslot; j++) if (needy[j]) {
+      int st = run(j, cur[j - 1].ex, &cur[j], &nw[j]); if (st > mx) mx = st;
+    }
+    /* speculation for the successors of the first needy slots, lanes permitting */
+    int nsl = 0;
+    for (int j = 0; j < nslot; j++) nsp[j] = 0;
+    if (spec) {
+      int budget = (lanes_cap - tot) / 5;
+      for (int j = 1; j + 1 < nslot && budget > 0; j++) if (needy[j]) {
+        budget--;
+        St o = cur[j].ex;
+        for (int bb = 0; bb < 6; bb++) {
+          if (bb == o.b) continue;
+          St e = o; e.b = bb;
+          int st = run(j + 1, e, &cur[j + 1], &sp[(size_t)(j + 1) * 6 + nsp[j + 1]]);
+          nsp[j + 1]++; nsl++;
+          if (st > mx) mx = st;
+        }
+      }
+    }
+    crit += mx;
+    for (int j = 1; j < nslot; j++) if (needy[j]) {
+      changed[j] = !eq(nw[j].ex, cur[j].ex);
+      if (changed[j]) { if (nw[j].ex.p == cur[j].ex.p && nw[j].ex.k == cur[j].ex.k) same_pk++; else diff_pk++; }
+      any_changed |= changed[j];
+      memo[j] = cur[j]; has_memo[j] = 1; cur[j] = nw[j];
+    }
+    if (!any_changed) break;
+  }
+  printf("S %ld slots %d ph1_steps %d rounds %d crit_steps %ld needy_avg %.1f memo_hits %d spec_hits %d changed_same_pk %ld diff_pk %ld\n", S, nslot,
+         ph1, rounds, crit, (double)needy_sum / rounds, memo_hits, spec_hits, same_pk, diff_pk);
+  return 0;
+}
