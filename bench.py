@@ -821,7 +821,8 @@ def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     cells, labels = make_cells("c2p", B, seed=1000 * rank)
     rb = ldt_amd.ResidentBatch(cells, labels, device=dev)
     pipe = ldt_amd.DecodePipeline(depth=7, device=dev, profile=True)
-    K = max(args.steps, 20)
+    # ~5 ms per batch 7 deep: at least 60 steps, so that fill and drain stay small
+    K = max(args.steps, 60)
     pipe.stage_times(reset=True)
     t = _warm_then_time(lambda: pipe.decode(rb), K, 15, 0.25, barrier, max_over_ranks)
     st = pipe.stage_times(reset=True)

@@ -335,31 +335,6 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
   // half (high) while k <= 48, the l1 half (low) from k = 49
   // (table offset and half come from the state, off the chain)
   const uint32_t soff = (slot << 13) + (st.k >= 49 ? 0u : 2u);
-#ifdef LDT_EXP_COUNT_V2
-  // index by one bit-field extract, address by one shift-add (written as
-  // asm: the compiler turns (pk >> 21) << 2 into a shift, a mask and a
-  // three-operand add, one more dependent VALU before the load)
-  uint32_t idx, addr;
-  asm("v_bfe_u32 %0, %1, 21, 11" : "=v"(idx) : "v"(pk));
-  static_assert(kLookBits == 11, "the asm extracts 11 bits");
-  const uint32_t base = (uint32_t)(uintptr_t)(dec.tabs + soff);
-  asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(addr) : "v"(idx), "v"(base));
-  const uint32_t e = *(lds_cu16)(uintptr_t)addr;
-  const uint32_t t = e & 31u;
-  nblk += dcs ? 1 : 0;
-  // a long code's entries (both halves: l1's indirect entry) have total 0
-  // and advance 0, so this step leaves the state as it is and the
-  // wave-uniform branch below, off the bit-position chain, decodes it
-  R.consume((int)t);
-  advance(st, dec, (int)(e >> 9));
-  if (__builtin_expect(__any(t == 0), 0)) {
-    if (t == 0) {
-      const uint32_t e2 = lookup_long(dec, slot, e, pk, st.b3, !dcs);
-      R.consume((int)(e2 & 31));
-      advance(st, dec, (int)(e2 >> 9));
-    }
-  }
-#else
   const uint32_t idx4 = (pk >> (32 - kLookBits)) << 2;
   const uint32_t e = *(lds_cu16)(dec.tabs + soff + idx4);
   uint32_t t = e & 31u;
@@ -374,7 +349,6 @@ __device__ __forceinline__ void count_step(Rd<W> &R, St &st, const Dec &dec, int
   nblk += dcs ? 1 : 0;
   R.consume((int)t);
   advance(st, dec, (int)adv);
-#endif
 }
 
 // Coefficients of a block are stored in zigzag (decode) order, int16 slots
@@ -699,88 +673,11 @@ struct Cp {
   int n;
 };
 
-#ifdef LDT_EXP_COUNT_V3
-// Count-mode state with the next lookup's table address kept in a register,
-// so that the step's second dependency chain (entry -> advance -> state ->
-// table slot -> address) is an add, a compare and two selects: base is the
-// LDS address of the half to read for (b3, k); acb the count half of block
-// b3's AC table; acbn / dcbn the AC count half and the DC table of the next
-// block (the selects at a block end take them; their successors are
-// computed from the old state, in the shadow of the lookup).
-struct CSt {
-  int b3, k;
-  uint32_t base, acb, acbn, dcbn;
-};
-__device__ __forceinline__ uint32_t half_addr(const Dec &dec, uint32_t seq, int b3) {
-  return (uint32_t)(uintptr_t)dec.tabs + (__builtin_amdgcn_ubfe(seq, (uint32_t)b3, 3u) << 13) + 2u;
-}
-__device__ __forceinline__ int next_b3(const Dec &dec, int b3) {
-  const int nb = b3 + 3;
-  return nb == dec.b3end ? 0 : nb;
-}
-__device__ __forceinline__ CSt make_cst(const Dec &dec, const St &st) {
-  CSt c;
-  c.b3 = st.b3;
-  c.k = st.k;
-  const int nb = next_b3(dec, st.b3);
-  c.acb = half_addr(dec, dec.acseq, st.b3);
-  c.acbn = half_addr(dec, dec.acseq, nb);
-  c.dcbn = half_addr(dec, dec.dcseq, nb);
-  c.base = st.k == 0 ? half_addr(dec, dec.dcseq, st.b3) : (st.k >= 49 ? c.acb - 2u : c.acb);
-  return c;
-}
-__device__ __forceinline__ void cst_advance(CSt &c, const Dec &dec, uint32_t adv, int nb, uint32_t acbnn,
-                                            uint32_t dcbnn) {
-  const int k2 = c.k + (int)adv;
-  const bool end = k2 >= 64;
-  c.base = end ? c.dcbn : (k2 >= 49 ? c.acb - 2u : c.acb);
-  c.k = end ? 0 : k2;
-  c.b3 = end ? nb : c.b3;
-  c.acb = end ? c.acbn : c.acb;
-  c.acbn = end ? acbnn : c.acbn;
-  c.dcbn = end ? dcbnn : c.dcbn;
-}
-template <class W>
-__device__ __forceinline__ void count_step3(Rd<W> &R, CSt &c, const Dec &dec, int &nblk) {
-  const uint32_t pk = R.peek();
-  uint32_t idx, addr;
-  asm("v_bfe_u32 %0, %1, 21, 11" : "=v"(idx) : "v"(pk));
-  asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(addr) : "v"(idx), "v"(c.base));
-  const uint32_t e = *(lds_cu16)(uintptr_t)addr;
-  // from the old state, while the lookup is in flight
-  const int nb = next_b3(dec, c.b3), nnb = next_b3(dec, nb);
-  const uint32_t acbnn = half_addr(dec, dec.acseq, nnb), dcbnn = half_addr(dec, dec.dcseq, nnb);
-  const bool dcs = c.k == 0;
-  const uint32_t t = e & 31u;
-  nblk += dcs ? 1 : 0;
-  // a long code's entries have total 0 and advance 0: the state stays and
-  // the wave-uniform branch below decodes the symbol
-  R.consume((int)t);
-  cst_advance(c, dec, e >> 9, nb, acbnn, dcbnn);
-  if (__builtin_expect(__any(t == 0), 0)) {
-    if (t == 0) {
-      const uint32_t slot = __builtin_amdgcn_ubfe(dcs ? dec.dcseq : dec.acseq, (uint32_t)c.b3, 3u);
-      const uint32_t e2 = lookup_long(dec, slot, e, pk, c.b3, !dcs);
-      R.consume((int)(e2 & 31));
-      cst_advance(c, dec, e2 >> 9, nb, acbnn, dcbnn);
-    }
-  }
-}
-template <class W>
-__device__ __forceinline__ void count_until(Rd<W> &R, int32_t lim, St &st, const Dec &dec,
-                                            int &nblk) {
-  CSt c = make_cst(dec, st);
-  while (R.p < lim) count_step3(R, c, dec, nblk);
-  st.b3 = c.b3;
-  st.k = c.k;
-}
-#else
 template <class W>
 __device__ __forceinline__ void count_until(Rd<W> &R, int32_t lim, St &st, const Dec &dec,
                                             int &nblk) {
   while (R.p < lim) count_step(R, st, dec, nblk);
 }
-#endif
 
 // COUNT decode from the reader's position to the first boundary >= stop
 // (positions in reader coordinates), recording the checkpoints. COMPARE: stop

@@ -123,6 +123,29 @@ int main(int argc, char **argv) {
     if (!tot) break;
     needy_sum += tot;
     int mx = 0, any_changed = 0;
+    if (spec == 2) {
+      /* chain following: a needy slot's lane continues into its successor
+       * while its exit changed and the successor is not in this round's
+       * work list (that slot's own lane re-decodes it from the snapshot) */
+      Traj *snap = calloc(nslot, sizeof(Traj));
+      memcpy(snap, cur, sizeof(Traj) * nslot);
+      for (int j = 1; j < nslot; j++) if (needy[j]) {
+        int st = run(j, snap[j - 1].ex, &cur[j], &nw[j]);
+        int q = j;
+        while (!eq(nw[q].ex, cur[q].ex) && q + 1 < nslot && !needy[q + 1]) {
+          memo[q] = cur[q]; has_memo[q] = 1; cur[q] = nw[q];
+          q++;
+          if (eq(cur[q - 1].ex, cur[q].en)) break;
+          if (has_memo[q] && eq(memo[q].en, cur[q - 1].ex)) { Traj t = cur[q]; cur[q] = memo[q]; cur[q].ncp = 0; memo[q] = t; memo_hits++; continue; }
+          st += run(q, cur[q - 1].ex, &cur[q], &nw[q]);
+          needy_sum++;
+        }
+        if (st > mx) mx = st;
+        if (q != j || 1) { /* the last decoded slot is applied below with the others */ }
+        needy[q] = 1;
+      }
+      free(snap);
+    } else
     for (int j = 1; j < nslot; j++) if (needy[j]) {
       int st = run(j, cur[j - 1].ex, &cur[j], &nw[j]); if (st > mx) mx = st;
     }
