@@ -101,17 +101,6 @@ template <bool SKEW = true> __device__ __forceinline__ int skw(int x) {
   return SKEW ? x + ((x >> 5) << 2) : x;
 }
 
-// The 4:2:0 fast path's staging rows (SRC 0/5) in blocks of 32 pixels, each
-// followed by a copy of the next block's first 6 pixels and 2 dwords of pad:
-// a horizontal window (KS <= 7 taps) never leaves its block, so its taps are
-// one base address plus immediate offsets (no per-tap select, which the raw
-// rows' skew needs and which cost 44 VGPRs here), and a stride of 40 dwords
-// puts the taps of the 32 lanes of a ds_read_b32 group on at most 2 banks for
-// 512- and 500-pixel sources (3 unblocked: scale 16/7 maps lanes 14 apart to
-// one bank). Blocks stay 16-byte aligned.
-constexpr int kHaloBlk = 32, kHaloStride = 40;
-__device__ __forceinline__ int hal(int x) { return (x >> 5) * kHaloStride + (x & (kHaloBlk - 1)); }
-
 // 16 packed RGB pixels -> 16 RGBx dwords at pixels [x0, x0+16) of a staging
 // row. The byte above B is left as whatever follows (the taps read bytes 0..2).
 template <bool SKEW>
@@ -259,12 +248,12 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
                                              const int32_t *__restrict__ status, const Geom4 &g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // Skewed staging for raw rows (c5: 4-5-way tap conflicts otherwise, and the
-  // kernel is LDS-bound). The 4:2:0 fast path's rows are blocked (hal): the
-  // skew's per-tap selects cost 44 VGPRs there (2 waves per SIMD instead of
-  // 3, standalone 0.153 -> 0.175 ms at c2); generic JPEG rows stay plain.
+  // kernel is LDS-bound). JPEG rows stay plain (the
+  // skew's per-tap selects took k_resize4<5,7> to 190 VGPRs, 2 waves per
+  // SIMD, 0.153 -> 0.175 ms at c2 with half the bank conflicts; blocked rows
+  // with a halo copy, 2-way banks at 148 VGPRs, measured 0.155 vs 0.152 ms).
   constexpr bool kJpeg = SRC == 0 || SRC == 2 || SRC == 5;
   constexpr bool kSkew = !kJpeg;
-  constexpr bool kHalo = SRC == 0 || SRC == 5; // the blocked 4:2:0 staging (hal)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float *s_lut = reinterpret_cast<float *>(smem);
   for (int i = tid; i < 768; i += (int)blockDim.x) s_lut[i] = lut[i];
@@ -322,7 +311,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   int xsk[4], xcr[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    xsk[q] = kHalo ? hal(xm[q]) : skw<kSkew>(xm[q]);
+    xsk[q] = skw<kSkew>(xm[q]);
     xcr[q] = 32 - (xm[q] & 31);
   }
   // band source rows
@@ -443,16 +432,9 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
             px[j] = __builtin_amdgcn_perm(xb, __builtin_amdgcn_perm(xg, xr, 0x0C0C0602u), 0x0C060100u);
           }
           if (x0 < W) {
-            uint32_t *sr = r ? s1 : s0;
-            uint4 *dq = reinterpret_cast<uint4 *>(sr + (kHalo ? hal(x0) : skw<kSkew>(x0)));
+            uint4 *dq = reinterpret_cast<uint4 *>((r ? s1 : s0) + x0);
             dq[0] = make_uint4(px[0], px[1], px[2], px[3]);
             dq[1] = make_uint4(px[4], px[5], px[6], px[7]);
-            if (kHalo && (x0 & (kHaloBlk - 1)) == 0 && x0 > 0) {
-              // the previous block's copy of this block's first 6 pixels
-              uint32_t *h = sr + hal(x0 - kHaloBlk) + kHaloBlk;
-              *reinterpret_cast<uint4 *>(h) = make_uint4(px[0], px[1], px[2], px[3]);
-              *reinterpret_cast<uint2 *>(h + 4) = make_uint2(px[4], px[5]);
-            }
           }
         }
         (void)d;
@@ -491,19 +473,12 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
           p1[j] = ycc_px((int)((yb_ >> sh) & 255), cb[1][j], crr[1][j]);
         }
         if (x0 < W) {
-          uint4 *d0 = reinterpret_cast<uint4 *>(s0 + (kHalo ? hal(x0) : skw<kSkew>(x0)));
-          uint4 *d1 = reinterpret_cast<uint4 *>(s1 + (kHalo ? hal(x0) : skw<kSkew>(x0)));
+          uint4 *d0 = reinterpret_cast<uint4 *>(s0 + skw<kSkew>(x0));
+          uint4 *d1 = reinterpret_cast<uint4 *>(s1 + skw<kSkew>(x0));
           d0[0] = make_uint4(p0[0], p0[1], p0[2], p0[3]);
           d0[1] = make_uint4(p0[4], p0[5], p0[6], p0[7]);
           d1[0] = make_uint4(p1[0], p1[1], p1[2], p1[3]);
           d1[1] = make_uint4(p1[4], p1[5], p1[6], p1[7]);
-          if (kHalo && (x0 & (kHaloBlk - 1)) == 0 && x0 > 0) {
-            uint32_t *h0 = s0 + hal(x0 - kHaloBlk) + kHaloBlk, *h1 = s1 + hal(x0 - kHaloBlk) + kHaloBlk;
-            *reinterpret_cast<uint4 *>(h0) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
-            *reinterpret_cast<uint2 *>(h0 + 4) = make_uint2(p0[4], p0[5]);
-            *reinterpret_cast<uint4 *>(h1) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
-            *reinterpret_cast<uint2 *>(h1 + 4) = make_uint2(p1[4], p1[5]);
-          }
         }
       } else {
         // generic: any supported sampling, gray, RGB, wide images
@@ -568,8 +543,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
         // Pillow weights are >= 0 and <= 2^22: 24-bit products (v_mul_u32_u24
         // with SDWA byte selects), exact in 32 bits. The window crosses at
         // most one 32-pixel skew step (KS < 32), at tap xcr[q].
-        const uint32_t v = kSkew ? (rowp + (t < xcr[q] ? xsk[q] : xsk[q] + 4))[t]
-                                 : (kHalo ? rowp[xsk[q] + t] : rowp[xm[q] + t]);
+        const uint32_t v = kSkew ? (rowp + (t < xcr[q] ? xsk[q] : xsk[q] + 4))[t] : rowp[xm[q] + t];
         const uint32_t kw = (uint32_t)wgt[q][t];
         a0 += (int32_t)__umul24(v & 255, kw);
         a1 += (int32_t)__umul24((v >> 8) & 255, kw);
@@ -674,16 +648,13 @@ static int wave_bytes4(const Geom4 &g) {
   return (b + 15) & ~15;
 }
 
-// jpeg: the launches of a JPEG batch, whose 4:2:0 fast-path rows use the
-// blocked layout (hal) and the others the plain one: room for both
 static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g,
-                       int wpg = kResizeWaves, bool jpeg = false) {
+                       int wpg = kResizeWaves) {
   g.wpg = wpg;
   g.ks_v = resample_ksize_host(max_h, kOut);
   g.ring = g.ks_v + 1; // an output row is finished within 2 rows of its window end
   const int px = ((max_w + 15) / 16) * 16 + ks_h + 16;
   g.spad = (px + ((px >> 5) << 2) + 4 + 3) & ~3; // skewed pixels (skw)
-  if (jpeg) g.spad = std::max(g.spad, (px + kHaloBlk - 1) / kHaloBlk * kHaloStride);
   g.wave_bytes = wave_bytes4(g);
   int nb = (waves_target + n - 1) / n;
   if (nb < 1) nb = 1;
@@ -747,8 +718,8 @@ bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t
   const int ks_h = resample_ksize_host(p.max_w, kOut);
   if (ks_h > 11) return false;
   const int wpg = p.resize_wpg > 0 ? p.resize_wpg : kResizeWaves;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, wpg, true)) return false;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g, wpg, true)) return false;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, wpg)) return false;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g, wpg)) return false;
   RawSrc raw{nullptr, 0, 0, 0};
   // fast-path images and the rest go to separate kernels (each skips the
   // other's images); a batch of one kind launches one kernel. The first
