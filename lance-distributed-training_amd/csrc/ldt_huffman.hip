@@ -1260,11 +1260,6 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff_image(
     int16_t *__restrict__ coef, uint32_t *__restrict__ brec, uint32_t *__restrict__ bcarry,
     int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
   __shared__ ImgLds sh;
-#ifdef LDT_HUFF_PRIO
-  // experiment: the decoder's waves ahead of co-resident kernels' waves
-  // (resize / IDCT of the other batches in flight) in instruction issue
-  __builtin_amdgcn_s_setprio(LDT_HUFF_PRIO);
-#endif
   const int img = par_img[blockIdx.x];
   if (status[img] != 0) return;
   const ImgDesc &d = descs[img];
