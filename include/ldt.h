@@ -91,6 +91,11 @@ extern "C" {
                                  stamps, rounds, symbols) into the plan blob,
                                  read with ldt_debug_counters; 0 (default): no
                                  counters (their atomics cost kernel time)     */
+#define LDT_OPT_HUFF_WINDOW 17 /* cap in bytes on the parallel Huffman decoder's
+                                 LDS stream window (-1, the default: what the
+                                 CU's LDS leaves; 0: every stream read from
+                                 global memory, destuffed by k_destuff_*) --
+                                 a study knob                  */
 #define LDT_OPT_RESIZE_WG_WAVES 15 /* waves (one band each) per k_resize4
                                  workgroup for JPEG sources: 0 default (2),
                                  1, 2 or 4; a 1-wave workgroup (~14 KB of LDS

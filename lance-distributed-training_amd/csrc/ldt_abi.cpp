@@ -92,6 +92,7 @@ struct ldt_ctx {
   hipStream_t copy_stream = nullptr; // ldt_set_copy_stream: replaces the device's copy stream (mode 0)
   bool host_timing = false;
   bool debug_counters = false; // LDT_OPT_DEBUG_COUNTERS
+  int64_t win_cap = -1;        // LDT_OPT_HUFF_WINDOW: cap on k_huff_image's LDS window (bytes; -1 none)
   CopyPlacement placement; // of the current pool
   static constexpr int kSlots = 2;
   // device cells, one buffer per pinned slot: a copy-stream DMA into one may
@@ -802,7 +803,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   // destuff_into_window); those images get no destuff chunks (ds_count 0)
   int n_ds_img = 0; // baseline images left to k_destuff_*
   {
-    const int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs);
+    int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs);
+    if (c->win_cap >= 0) cap = std::min<int64_t>(cap, c->win_cap);
     const int64_t winb = std::min<int64_t>(max_window, cap) & ~(int64_t)15;
     chunk_img.clear();
     n_chunks = 0;
@@ -959,7 +961,8 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   {
     // LDS window of k_huff_image: the largest image's stream, capped by what
     // is left of the CU's LDS after the tables (bigger streams read global)
-    const int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs);
+    int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs);
+    if (c->win_cap >= 0) cap = std::min<int64_t>(cap, c->win_cap);
     p.win_bytes = (int)(std::min<int64_t>(max_window, cap) & ~(int64_t)15);
   }
   p.warm_pct = c->warm_pct;
@@ -1199,6 +1202,10 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
   case LDT_OPT_SYNC_WARM:
     if (value < 0 || value > 200) return set_err(c, LDT_ERR_ARG, "sync warm-up %lld", (long long)value);
     c->warm_pct = (int)value;
+    return LDT_OK;
+  case LDT_OPT_HUFF_WINDOW:
+    if (value < -1 || value > kHuffLdsMax) return set_err(c, LDT_ERR_ARG, "window cap %lld", (long long)value);
+    c->win_cap = value;
     return LDT_OK;
   case LDT_OPT_DEBUG_COUNTERS:
     c->debug_counters = value != 0;

@@ -61,6 +61,7 @@ OPT_COPY_BIND = 13
 OPT_COPY_NT = 14
 OPT_RESIZE_WG_WAVES = 15
 OPT_DEBUG_COUNTERS = 16
+OPT_HUFF_WINDOW = 17
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
 HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status", "copy_wake", "copy_span")
