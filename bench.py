@@ -318,7 +318,7 @@ def main():
         bytes_per_img = 1024 * 1024 * 3 + OUT_BYTES
 
         def step():
-            return ldt_amd.resize_raw(raw, 1024, 1024, normalize=True)
+            return ldt_amd.resize_raw(raw, 1024, 1024, device=dev, normalize=True)
     else:
         nb = 2  # two distinct batches, alternated
         batches, host_batches = [], []
@@ -653,8 +653,9 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
 
     copy = args.dataset_copy if copy is None else copy
     # the dataset rank 0 writes holds every rank's rows: per-rank batches
-    # shrink with the world size (at least 12) so that it stays ~1.7 GB at c2
-    nbatch = max(12, args.dataset_batches // world)
+    # shrink with the world size (at least 12, or the whole request when that
+    # is smaller) so that it stays ~1.7 GB at c2
+    nbatch = max(min(12, args.dataset_batches), args.dataset_batches // world)
     # FOOD101's fragments [12500 x 6, 750] (create_datasets/classification.py:16,60)
     # scaled so that a rank reads about `nbatch` batches
     if wl["sampler"] == "fragment":
@@ -768,7 +769,7 @@ def leg_c5(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     ctx.set_option(_lib.OPT_PROFILE, 1)
     K = max(args.steps, 20)
     ctx.stage_times(reset=True)
-    t = _warm_then_time(lambda: ldt_amd.resize_raw(raw, H, W, normalize=True), K, 3, 0.25, barrier, max_over_ranks)
+    t = _warm_then_time(lambda: ldt_amd.resize_raw(raw, H, W, device=dev, normalize=True), K, 3, 0.25, barrier, max_over_ranks)
     st = ctx.stage_times(reset=True)
     bpi = H * W * 3 + OUT_BYTES
     ms, n = st["resize"]
@@ -790,7 +791,7 @@ def leg_c5(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
         leg["roofline"]["traffic_source"] = tr.get("source")
     if world == 1:
         host = raw.cpu()
-        th = _warm_then_time(lambda: ldt_amd.resize_raw(host, H, W, normalize=True), 3, 1, 0.0, barrier,
+        th = _warm_then_time(lambda: ldt_amd.resize_raw(host, H, W, device=dev, normalize=True), 3, 1, 0.0, barrier,
                              max_over_ranks)
         leg["value_host_input"] = round(B * 3 / th, 1)
         leg["value_host_input_note"] = ("pageable host uint8 [1024,1024,1024,3] -> ldt_resize_raw: pinned "

@@ -76,7 +76,9 @@ def test_bench_multi_rank_rehearsal(ranks):
                         os.path.join(REPO, "bench.py"), "--gpus", str(ranks), "--steps", "3", "--warmup", "1",
                         "--no-cpu-baseline", "--dataset-batches", "2", "--dataset-epochs", "1", "--host-reps", "1"],
                        cwd=REPO, capture_output=True, text=True, timeout=840, env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
+    # the ranks' own tracebacks first (torchrun's summary follows them)
+    assert r.returncode == 0, "\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[rank"))[-3000:] \
+        + r.stderr[-1000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
