@@ -103,6 +103,11 @@ int main(int argc, char **argv) {
   long same_pk = 0, diff_pk = 0;
   long crit = 0; int rounds = 0, spec_hits = 0, memo_hits = 0, needy_sum = 0;
   Traj *nw = calloc(nslot, sizeof(Traj)); int *needy = calloc(nslot, sizeof(int)); int *changed = calloc(nslot, sizeof(int));
+  /* ANALYSE=1: every round's entries (after the adoption loop), compared
+   * with the converged ones at the end */
+  const int analyse = getenv("ANALYSE") != NULL;
+  St *snap_en = analyse ? calloc((size_t)nslot * 64, sizeof(St)) : NULL;
+  int *snap_need = analyse ? calloc((size_t)nslot * 64, sizeof(int)) : NULL;
   for (;;) {
     rounds++;
     /* adoption loop: memo and speculation hits, until none */
@@ -120,6 +125,8 @@ int main(int argc, char **argv) {
     }
     int tot = 0;
     for (int j = 1; j < nslot; j++) { needy[j] = !eq(cur[j - 1].ex, cur[j].en); tot += needy[j]; }
+    if (analyse && rounds <= 64)
+      for (int j = 0; j < nslot; j++) { snap_en[(size_t)(rounds - 1) * nslot + j] = cur[j].en; snap_need[(size_t)(rounds - 1) * nslot + j] = j ? needy[j] : 0; }
     if (!tot) break;
     needy_sum += tot;
     int mx = 0, any_changed = 0;
@@ -174,6 +181,19 @@ int main(int argc, char **argv) {
       memo[j] = cur[j]; has_memo[j] = 1; cur[j] = nw[j];
     }
     if (!any_changed) break;
+  }
+  if (analyse) {
+    /* per round: needy slots, non-needy slots whose entry is already the
+     * converged one (a write started then would stand), non-needy ones whose
+     * entry still changes, and the final prefix (slots before the first needy) */
+    for (int r = 0; r < rounds && r < 64; r++) {
+      int nn = 0, good = 0, bad = 0, pre = nslot;
+      for (int j = 0; j < nslot; j++) {
+        if (snap_need[(size_t)r * nslot + j]) { nn++; if (pre == nslot) pre = j; continue; }
+        if (eq(snap_en[(size_t)r * nslot + j], cur[j].en)) good++; else bad++;
+      }
+      printf("round %d needy %d stable %d unstable %d prefix %d\n", r + 1, nn, good, bad, pre);
+    }
   }
   printf("S %ld slots %d ph1_steps %d rounds %d crit_steps %ld needy_avg %.1f memo_hits %d spec_hits %d changed_same_pk %ld diff_pk %ld\n", S, nslot,
          ph1, rounds, crit, (double)needy_sum / rounds, memo_hits, spec_hits, same_pk, diff_pk);
