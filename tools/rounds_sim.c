@@ -42,6 +42,7 @@ static int decode(const Tab *t, long *p) {
   *p += 16; return 0;
 }
 static const int bcomp[6] = {0, 0, 0, 0, 1, 2};
+static const int bcount = 6;
 typedef struct { long p; int b, k; } St;
 static void step(St *s) {
   int c = bcomp[s->b];
@@ -51,6 +52,18 @@ static void step(St *s) {
     if (t) { s->k += r + 1; s->p += t; } else s->k = (r == 15) ? s->k + 16 : 64;
     if (s->k >= 64) { s->k = 0; s->b = (s->b + 1) % 6; }
   }
+}
+/* step() that also reports a symbol no valid stream holds: a code the table
+ * lacks, or an AC value or ZRL past coefficient 63 */
+static int bad_step(St *s) {
+  int c = bcomp[s->b];
+  if (s->k == 0) { long p0 = s->p; int t = decode(&dc[cdc[c]], &s->p); int bad = s->p - p0 == 16 && t == 0; s->p += t; s->k = 1; return bad || t > 11; }
+  long p0 = s->p;
+  int rs = decode(&ac[cac[c]], &s->p); int r = rs >> 4, t = rs & 15;
+  int bad = s->p - p0 == 16 && rs == 0;
+  if (t) { s->k += r + 1; bad |= s->k > 63; s->p += t; } else if (r == 15) { s->k += 16; bad |= s->k > 63; } else s->k = 64;
+  if (s->k >= 64) { s->k = 0; s->b = (s->b + 1) % 6; }
+  return bad;
 }
 static int eq(St a, St b) { return a.p == b.p && a.b == b.b && a.k == b.k; }
 
@@ -99,7 +112,27 @@ int main(int argc, char **argv) {
   /* speculation results: per slot, up to 6 (entry, traj) */
   Traj *sp = calloc((size_t)nslot * 6, sizeof(Traj)); int *nsp = calloc(nslot, sizeof(int));
   int ph1 = 0;
-  for (int j = 0; j < nslot; j++) { St e = {(long)j * S, 0, 0}; int st = run(j, e, NULL, &cur[j]); if (st > ph1) ph1 = st; }
+  /* GUESS=<bits>: the phase-1 block phase per slot from a test decode of
+   * every b over the first <bits> of the range: the b with the fewest
+   * impossible symbols (first such symbol latest on a tie) */
+  const long glen = getenv("GUESS") ? atol(getenv("GUESS")) : 0;
+  long guess_steps = 0; int guess_right = 0;
+  for (int j = 0; j < nslot; j++) {
+    St e = {(long)j * S, 0, 0};
+    if (glen > 0 && j > 0) {
+      int best_b = 0, best_bad = 1 << 30; long best_first = -1;
+      for (int bb = 0; bb < bcount; bb++) {
+        St t = {(long)j * S, bb, 0}; int nbad = 0; long first = -1;
+        while (t.p < (long)j * S + glen && t.p < nbitsl) { if (bad_step(&t)) { nbad++; if (first < 0) first = t.p; } guess_steps++; }
+        if (first < 0) first = 1L << 40;
+        if (nbad < best_bad || (nbad == best_bad && first > best_first)) { best_bad = nbad; best_b = bb; best_first = first; }
+      }
+      e.b = best_b;
+    }
+    int st = run(j, e, NULL, &cur[j]); if (st > ph1) ph1 = st;
+  }
+  St *ph1_ex = malloc(sizeof(St) * nslot);
+  for (int j = 0; j < nslot; j++) ph1_ex[j] = cur[j].ex;
   long same_pk = 0, diff_pk = 0;
   long crit = 0; int rounds = 0, spec_hits = 0, memo_hits = 0, needy_sum = 0;
   Traj *nw = calloc(nslot, sizeof(Traj)); int *needy = calloc(nslot, sizeof(int)); int *changed = calloc(nslot, sizeof(int));
@@ -181,6 +214,35 @@ int main(int argc, char **argv) {
       memo[j] = cur[j]; has_memo[j] = 1; cur[j] = nw[j];
     }
     if (!any_changed) break;
+  }
+  {
+    int right = 0, right_b = 0;
+    for (int j = 0; j < nslot; j++) { right += eq(ph1_ex[j], cur[j].ex); right_b += ph1_ex[j].b == cur[j].ex.b; }
+    printf("phase-1 exits already final: %d of %d (block phase right: %d)\n", right, nslot, right_b);
+  }
+  if (getenv("WAVES")) {
+    /* write-pass balance: symbols each slot's lane decodes from its true
+     * entry to its exit (stop at the range end with the block complete, as
+     * write_run), summed per 64-slot wave as the wave's slowest lane, for the
+     * slots in order, sorted by their symbols, and sorted by their blocks */
+    int *sym = calloc(nslot, sizeof(int)), *blk = calloc(nslot, sizeof(int)), *ord = calloc(nslot, sizeof(int));
+    long tot_sym = 0;
+    for (int j = 0; j < nslot; j++) {
+      St s = cur[j].en; long stop = (long)(j + 1) * S; if (stop > nbitsl) stop = nbitsl;
+      int n = 0, nb = 0;
+      while (s.p < stop || s.k != 0) { if (s.k == 0) nb++; step(&s); n++; if (s.p >= nbitsl + 64) break; }
+      sym[j] = n; blk[j] = nb; tot_sym += n;
+    }
+    for (int mode = 0; mode < 3; mode++) {
+      for (int j = 0; j < nslot; j++) ord[j] = j;
+      if (mode) for (int a = 0; a < nslot; a++) for (int b = a + 1; b < nslot; b++) {
+        int ka = mode == 1 ? sym[ord[a]] : blk[ord[a]], kb = mode == 1 ? sym[ord[b]] : blk[ord[b]];
+        if (kb > ka) { int t = ord[a]; ord[a] = ord[b]; ord[b] = t; }
+      }
+      long summax = 0;
+      for (int w = 0; w * 64 < nslot; w++) { int m = 0; for (int l = w * 64; l < nslot && l < w * 64 + 64; l++) if (sym[ord[l]] > m) m = sym[ord[l]]; summax += m; }
+      printf("waves mode %s sum_of_wave_max %ld (avg-lane bound %.0f)\n", mode == 0 ? "in-order" : mode == 1 ? "by-symbols" : "by-blocks", summax, (double)tot_sym / 64.0);
+    }
   }
   if (analyse) {
     /* per round: needy slots, non-needy slots whose entry is already the
