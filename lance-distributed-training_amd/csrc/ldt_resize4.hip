@@ -629,13 +629,8 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   vertical(yb + 1);
 }
 
-#ifdef LDT_RESIZE_WAVES_PER_EU
-#define LDT_RESIZE_ATTR __attribute__((amdgpu_waves_per_eu(LDT_RESIZE_WAVES_PER_EU, 8)))
-#else
-#define LDT_RESIZE_ATTR
-#endif
 template <int SRC, int KS>
-__global__ void __launch_bounds__(256) LDT_RESIZE_ATTR k_resize4(const ImgDesc *__restrict__ descs,
+__global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ descs,
                                                  const uint8_t *__restrict__ planes, RawSrc raw,
                                                  const float *__restrict__ lut,
                                                  const int64_t *__restrict__ labels,
