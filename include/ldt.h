@@ -97,10 +97,9 @@ extern "C" {
                                  global memory, destuffed by k_destuff_*) --
                                  a study knob                  */
 #define LDT_OPT_RESIZE_WG_WAVES 15 /* waves (one band each) per k_resize4
-                                 workgroup for JPEG sources: 0 default (2),
-                                 1, 2 or 4; a 1-wave workgroup (~14 KB of LDS
-                                 at 512 px) fits beside a k_huff_image
-                                 workgroup of another batch on its CU      */
+                                 workgroup for JPEG sources: 0 default (4),
+                                 1, 2 or 4 (tuning knob: 4 keeps 12 waves
+                                 per CU at 512 px)           */
 #define LDT_OPT_FUSED_DESTUFF 11 /* 1 (default): the parallel Huffman decoder
                                  destuffs the scan bytes of an image whose
                                  stream fits its LDS window itself; 0: every

@@ -223,13 +223,19 @@ struct Geom4 {
   int wave_bytes;  // LDS per wave
   int fill;        // JPEG: this launch zero-fills failed images' bands (label -100)
   int wpg;         // waves (tasks) per workgroup
+  int rgbx;        // ring rows of RGBx dwords (JPEG sources) instead of three byte planes
 };
 
-constexpr int kKvRows = 16; // vertical coefficient rows cached per wave
-// Waves (tasks) per workgroup: two keep a workgroup's LDS (3 KB LUT + two
-// wave areas, ~24 KB at 512 px) small enough to share a CU with the Huffman
-// decoder of another batch in flight.
+constexpr int kKvRows = 8; // vertical coefficient rows cached per wave
+// Waves (tasks) per workgroup. Raw sources: two. JPEG sources: four, which
+// hold 12 waves per CU with the RGBx ring (3 KB LUT + 4 x 11.5 KB at 512 px:
+// 3 workgroups; 2-wave workgroups of 26 KB fit only 5 per CU and measured
+// 0.183 vs 0.150 ms standalone, profiles/r5/resize_rgbx_wg_r5wg.txt). No
+// resize workgroup shares a CU with a k_huff_image workgroup usefully: one
+// that fits (1 wave, <= 128 VGPRs) slows the decoder's rounds more than it
+// gains (profiles/r5/resize_coresident_ab_r5co.txt).
 constexpr int kResizeWaves = 2;
+constexpr int kResizeWavesJpeg = 4;
 
 // SRC: 0 JPEG planes, 4:2:0 fast staging (resize_fast420 images only);
 // 2 JPEG planes, generic staging (the other images); 1 raw HWC rows, 16-byte
@@ -289,8 +295,13 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
 
   uint8_t *wbase = smem + 3072 + wave * g.wave_bytes;
   uint32_t *stg = reinterpret_cast<uint32_t *>(wbase);               // 2 * spad dwords
-  uint8_t *ring = wbase + 8 * g.spad;                                // 3 * ring * 224
-  int32_t *kv = reinterpret_cast<int32_t *>(ring + 3 * g.ring * kOut); // kKvRows * ks_v
+  // the intermediate ring: JPEG sources keep RGBx dwords per column (one
+  // 4-byte store per column and row, one 16-byte read of 4 columns per
+  // vertical tap); raw sources three byte planes (their larger rings would
+  // cost a workgroup per CU as dwords)
+  constexpr bool kRgbx = kJpeg;
+  uint8_t *ring = wbase + 8 * g.spad;                                // (kRgbx ? 4 : 3) * ring * 224
+  int32_t *kv = reinterpret_cast<int32_t *>(ring + (kRgbx ? 4 : 3) * g.ring * kOut); // kKvRows * ks_v
   int32_t *vb = kv + kKvRows * g.ks_v;                               // kKvRows * 2
   const int ks_v = g.ks_v, RING = g.ring;
 
@@ -550,10 +561,16 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
         a2 += (int32_t)__umul24((v >> 16) & 255, kw);
       }
       const int sl = r ? slot1 : slot;
-      uint8_t *rw = ring + sl * kOut + ox;
-      rw[0] = (uint8_t)min((uint32_t)a0 >> kPrecisionBits, 255u);
-      rw[RING * kOut] = (uint8_t)min((uint32_t)a1 >> kPrecisionBits, 255u);
-      rw[2 * RING * kOut] = (uint8_t)min((uint32_t)a2 >> kPrecisionBits, 255u);
+      if constexpr (kRgbx) {
+        reinterpret_cast<uint32_t *>(ring)[sl * kOut + ox] =
+            min((uint32_t)a0 >> kPrecisionBits, 255u) | (min((uint32_t)a1 >> kPrecisionBits, 255u) << 8) |
+            (min((uint32_t)a2 >> kPrecisionBits, 255u) << 16);
+      } else {
+        uint8_t *rw = ring + sl * kOut + ox;
+        rw[0] = (uint8_t)min((uint32_t)a0 >> kPrecisionBits, 255u);
+        rw[RING * kOut] = (uint8_t)min((uint32_t)a1 >> kPrecisionBits, 255u);
+        rw[2 * RING * kOut] = (uint8_t)min((uint32_t)a2 >> kPrecisionBits, 255u);
+      }
     }
     slot = slot1 + 1 == RING ? 0 : slot1 + 1;
   };
@@ -577,6 +594,41 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
       if (ymin + cnt > done) break;
       ++next_oy;
       int s0 = (ymin - ya0) % RING;
+      if constexpr (kRgbx) {
+        // lane g < 56: output columns 4g..4g+3, all three channels, from one
+        // 16-byte read of the ring row per tap (lanes 56-63 read group 55)
+        const int gq = min(lane, 55);
+        int32_t acc[3][4];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][e] = 1 << (kPrecisionBits - 1);
+        for (int t = 0; t < cnt; ++t) {
+          const uint32_t kw = (uint32_t)__builtin_amdgcn_readfirstlane(kv[jr * ks_v + t]);
+          const int sl = s0 + t < RING ? s0 + t : s0 + t - RING;
+          const uint4 v4 = *reinterpret_cast<const uint4 *>(ring + (sl * kOut + 4 * gq) * 4);
+          const uint32_t w4[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[0][e] += (int32_t)__umul24(w4[e] & 255, kw);
+            acc[1][e] += (int32_t)__umul24((w4[e] >> 8) & 255, kw);
+            acc[2][e] += (int32_t)__umul24((w4[e] >> 16) & 255, kw);
+          }
+        }
+        if (lane < 56) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const float *lc = s_lut + i * 256;
+            float4 f;
+            f.x = lc[min((uint32_t)acc[i][0] >> kPrecisionBits, 255u)];
+            f.y = lc[min((uint32_t)acc[i][1] >> kPrecisionBits, 255u)];
+            f.z = lc[min((uint32_t)acc[i][2] >> kPrecisionBits, 255u)];
+            f.w = lc[min((uint32_t)acc[i][3] >> kPrecisionBits, 255u)];
+            *reinterpret_cast<float4 *>(out + (((int64_t)img * 3 + i) * kOut + oy0 + j) * kOut + 4 * lane) = f;
+          }
+        }
+        continue;
+      }
       int32_t acc[3][4];
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -644,17 +696,19 @@ __global__ void __launch_bounds__(256) k_resize4(const ImgDesc *__restrict__ des
 // Launch geometry.
 // ---------------------------------------------------------------------------
 static int wave_bytes4(const Geom4 &g) {
-  const int b = 8 * g.spad + 3 * g.ring * kOut + 4 * (kKvRows * g.ks_v + 2 * kKvRows);
+  const int b = 8 * g.spad + (g.rgbx ? 4 : 3) * g.ring * kOut + 4 * (kKvRows * g.ks_v + 2 * kKvRows);
   return (b + 15) & ~15;
 }
 
 static bool make_geom4(int n, int max_w, int max_h, int ks_h, int waves_target, Geom4 &g,
-                       int wpg = kResizeWaves) {
+                       int wpg = kResizeWaves, bool jpeg = false) {
   g.wpg = wpg;
+  g.rgbx = jpeg ? 1 : 0;
   g.ks_v = resample_ksize_host(max_h, kOut);
   g.ring = g.ks_v + 1; // an output row is finished within 2 rows of its window end
   const int px = ((max_w + 15) / 16) * 16 + ks_h + 16;
-  g.spad = (px + ((px >> 5) << 2) + 4 + 3) & ~3; // skewed pixels (skw)
+  // raw rows are skewed (skw); JPEG rows are not
+  g.spad = (px + (jpeg ? 0 : (px >> 5) << 2) + 4 + 3) & ~3;
   g.wave_bytes = wave_bytes4(g);
   int nb = (waves_target + n - 1) / n;
   if (nb < 1) nb = 1;
@@ -717,9 +771,9 @@ bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t
   Geom4 g;
   const int ks_h = resample_ksize_host(p.max_w, kOut);
   if (ks_h > 11) return false;
-  const int wpg = p.resize_wpg > 0 ? p.resize_wpg : kResizeWaves;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, wpg)) return false;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g, wpg)) return false;
+  const int wpg = p.resize_wpg > 0 ? p.resize_wpg : kResizeWavesJpeg;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, wpg, true)) return false;
+  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g, wpg, true)) return false;
   RawSrc raw{nullptr, 0, 0, 0};
   // fast-path images and the rest go to separate kernels (each skips the
   // other's images); a batch of one kind launches one kernel. The first
