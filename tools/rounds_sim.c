@@ -65,6 +65,31 @@ static int bad_step(St *s) {
   if (s->k >= 64) { s->k = 0; s->b = (s->b + 1) % 6; }
   return bad;
 }
+/* one count-mode step (ldt_plan.cpp count-mode entries, ldt_huffman.hip
+ * count_step): a DC symbol, or, while k <= 48, a run of AC symbols whose
+ * codes all lie in the 11 peeked bits (advance <= 15 before the last), else
+ * one AC symbol. Returns the symbols consumed. */
+static int code_len(const Tab *t, long p) {
+  uint32_t w = peek16(p);
+  for (int l = 1; l <= 16; l++) { int c = w >> (16 - l); if (c <= t->maxcode[l]) return l; }
+  return 16;
+}
+static int count_step_sim(St *s) {
+  if (s->k == 0 || s->k >= 49) { step(s); return 1; }
+  const long p0 = s->p; int n = 0, adv = 0;
+  for (;;) {
+    int c = bcomp[s->b];
+    St t = *s; step(&t); n++;
+    int a = t.k == 0 ? 64 : t.k - s->k; /* the symbol's coefficient advance (EOB: to the block end) */
+    *s = t; adv += a;
+    if (s->k == 0 || adv > 15) break;
+    long used = s->p - p0;
+    int cl = code_len(&ac[cac[bcomp[s->b]]], s->p);
+    if (used >= 11 || used + cl > 11) break;
+    (void)c;
+  }
+  return n;
+}
 static int eq(St a, St b) { return a.p == b.p && a.b == b.b && a.k == b.k; }
 
 typedef struct { St en, ex, cp[2]; int ncp; } Traj;
@@ -226,22 +251,28 @@ int main(int argc, char **argv) {
      * write_run), summed per 64-slot wave as the wave's slowest lane, for the
      * slots in order, sorted by their symbols, and sorted by their blocks */
     int *sym = calloc(nslot, sizeof(int)), *blk = calloc(nslot, sizeof(int)), *ord = calloc(nslot, sizeof(int));
+    int *cst = calloc(nslot, sizeof(int));
     long tot_sym = 0;
     for (int j = 0; j < nslot; j++) {
       St s = cur[j].en; long stop = (long)(j + 1) * S; if (stop > nbitsl) stop = nbitsl;
       int n = 0, nb = 0;
       while (s.p < stop || s.k != 0) { if (s.k == 0) nb++; step(&s); n++; if (s.p >= nbitsl + 64) break; }
       sym[j] = n; blk[j] = nb; tot_sym += n;
+      /* count-mode steps of the slot's phase-1 trajectory (from the guess) */
+      St c = {(long)j * S, 0, 0}; int ns = 0;
+      while (c.p < stop) { count_step_sim(&c); ns++; }
+      cst[j] = ns;
     }
-    for (int mode = 0; mode < 3; mode++) {
+    for (int mode = 0; mode < 4; mode++) {
       for (int j = 0; j < nslot; j++) ord[j] = j;
       if (mode) for (int a = 0; a < nslot; a++) for (int b = a + 1; b < nslot; b++) {
-        int ka = mode == 1 ? sym[ord[a]] : blk[ord[a]], kb = mode == 1 ? sym[ord[b]] : blk[ord[b]];
+        int ka = mode == 1 ? sym[ord[a]] : mode == 2 ? blk[ord[a]] : cst[ord[a]];
+        int kb = mode == 1 ? sym[ord[b]] : mode == 2 ? blk[ord[b]] : cst[ord[b]];
         if (kb > ka) { int t = ord[a]; ord[a] = ord[b]; ord[b] = t; }
       }
       long summax = 0;
       for (int w = 0; w * 64 < nslot; w++) { int m = 0; for (int l = w * 64; l < nslot && l < w * 64 + 64; l++) if (sym[ord[l]] > m) m = sym[ord[l]]; summax += m; }
-      printf("waves mode %s sum_of_wave_max %ld (avg-lane bound %.0f)\n", mode == 0 ? "in-order" : mode == 1 ? "by-symbols" : "by-blocks", summax, (double)tot_sym / 64.0);
+      printf("waves mode %s sum_of_wave_max %ld (avg-lane bound %.0f)\n", mode == 0 ? "in-order" : mode == 1 ? "by-symbols" : mode == 2 ? "by-blocks" : "by-phase1-count-steps", summax, (double)tot_sym / 64.0);
     }
   }
   if (analyse) {
