@@ -251,7 +251,7 @@ int main(int argc, char **argv) {
      * write_run), summed per 64-slot wave as the wave's slowest lane, for the
      * slots in order, sorted by their symbols, and sorted by their blocks */
     int *sym = calloc(nslot, sizeof(int)), *blk = calloc(nslot, sizeof(int)), *ord = calloc(nslot, sizeof(int));
-    int *cst = calloc(nslot, sizeof(int));
+    int *cst = calloc(nslot, sizeof(int)), *psym = calloc(nslot, sizeof(int));
     long tot_sym = 0;
     for (int j = 0; j < nslot; j++) {
       St s = cur[j].en; long stop = (long)(j + 1) * S; if (stop > nbitsl) stop = nbitsl;
@@ -259,20 +259,20 @@ int main(int argc, char **argv) {
       while (s.p < stop || s.k != 0) { if (s.k == 0) nb++; step(&s); n++; if (s.p >= nbitsl + 64) break; }
       sym[j] = n; blk[j] = nb; tot_sym += n;
       /* count-mode steps of the slot's phase-1 trajectory (from the guess) */
-      St c = {(long)j * S, 0, 0}; int ns = 0;
-      while (c.p < stop) { count_step_sim(&c); ns++; }
-      cst[j] = ns;
+      St c = {(long)j * S, 0, 0}; int ns = 0, nsym1 = 0;
+      while (c.p < stop) { nsym1 += count_step_sim(&c); ns++; }
+      cst[j] = ns; psym[j] = nsym1;
     }
-    for (int mode = 0; mode < 4; mode++) {
+    for (int mode = 0; mode < 5; mode++) {
       for (int j = 0; j < nslot; j++) ord[j] = j;
       if (mode) for (int a = 0; a < nslot; a++) for (int b = a + 1; b < nslot; b++) {
-        int ka = mode == 1 ? sym[ord[a]] : mode == 2 ? blk[ord[a]] : cst[ord[a]];
-        int kb = mode == 1 ? sym[ord[b]] : mode == 2 ? blk[ord[b]] : cst[ord[b]];
+        int ka = mode == 1 ? sym[ord[a]] : mode == 2 ? blk[ord[a]] : mode == 3 ? cst[ord[a]] : psym[ord[a]];
+        int kb = mode == 1 ? sym[ord[b]] : mode == 2 ? blk[ord[b]] : mode == 3 ? cst[ord[b]] : psym[ord[b]];
         if (kb > ka) { int t = ord[a]; ord[a] = ord[b]; ord[b] = t; }
       }
       long summax = 0;
       for (int w = 0; w * 64 < nslot; w++) { int m = 0; for (int l = w * 64; l < nslot && l < w * 64 + 64; l++) if (sym[ord[l]] > m) m = sym[ord[l]]; summax += m; }
-      printf("waves mode %s sum_of_wave_max %ld (avg-lane bound %.0f)\n", mode == 0 ? "in-order" : mode == 1 ? "by-symbols" : mode == 2 ? "by-blocks" : "by-phase1-count-steps", summax, (double)tot_sym / 64.0);
+      printf("waves mode %s sum_of_wave_max %ld (avg-lane bound %.0f)\n", mode == 0 ? "in-order" : mode == 1 ? "by-symbols" : mode == 2 ? "by-blocks" : mode == 3 ? "by-phase1-count-steps" : "by-phase1-symbols", summax, (double)tot_sym / 64.0);
     }
   }
   if (analyse) {
