@@ -1253,7 +1253,14 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   return true;
 }
 
-__global__ void __launch_bounds__(kHuffThreads) k_huff_image(
+// At most 80 VGPRs (6 waves per SIMD's worth): the decoder's 16 waves then
+// hold 4 x 80 of a SIMD's 512 registers, and two waves of k_idct (82) from
+// the other batches in flight fit beside them instead of one. k_idct uses no
+// LDS, so it shares the CU without slowing the decoder's LDS-bound rounds
+// (the resize does not: DESIGN.md §4), and the pipeline gains 4-5%
+// (profiles/r5/huff_vgpr_ab_r5h80.txt). The cap costs only SGPR spills to
+// VGPR lanes; at 72 VGPRs scratch spills begin.
+__global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ data,
     const uint8_t *__restrict__ dstuf, const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
