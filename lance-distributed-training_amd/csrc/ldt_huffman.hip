@@ -1113,11 +1113,9 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
 // uniform) for a corrupt image, with status 3 as k_destuff_layout sets it.
 // ---------------------------------------------------------------------------
 constexpr int kFuseTile = 16 * kHuffThreads;
-template <class Pre>
 __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ data, const ImgDesc &d,
                                                     LDS_AS uint8_t *win, ImgLds &sh, int tid,
-                                                    int32_t *__restrict__ status, int img,
-                                                    const Pre &after_first_load) {
+                                                    int32_t *__restrict__ status, int img) {
   // B0: the scan start rounded down to a word (pointer arithmetic on `data`
   // only, so the loads stay global loads rather than flat ones, which an LDS
   // wait would also wait for)
@@ -1207,7 +1205,6 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   // that: profiles/r4/huffvar_r4hv.txt)
   uint32_t wv[6], nx[6];
   load(0, wv);
-  after_first_load(); // the caller's table stores: their loads were issued first
   for (int64_t cb = 0; cb < span; cb += kFuseTile) {
     load(cb + kFuseTile, nx); // the next tile (clamped past the end)
     if (tile(cb, wv)) break;
@@ -1253,13 +1250,41 @@ __device__ __forceinline__ bool destuff_into_window(const uint8_t *__restrict__ 
   return true;
 }
 
+// The image's distinct tables into LDS by LDS-DMA (global_load_lds_dwordx4:
+// each wave instruction moves 64 x 16 B to one contiguous KB of LDS and holds
+// no VGPRs while in flight): the lc part of a slot is 8 such chunks, the l2
+// parts of two slots one chunk (their LDS areas are adjacent). The caller
+// waits (vmcnt 0) before the barrier that publishes them.
+__device__ __forceinline__ void stage_tables_dma(const HuffTab *__restrict__ htabs, const SlotTabs &st, int ns,
+                                                 LDS_AS uint8_t *tabs, int wave, int lane) {
+  const int nlc = ns * (kLcBytes / 1024);
+  const int nch = nlc + (ns + 1) / 2;
+  for (int c = wave; c < nch; c += kHuffThreads / 64) {
+    if (c < nlc) {
+      const int sl = c / (kLcBytes / 1024), k = c % (kLcBytes / 1024);
+      const uint8_t *src = reinterpret_cast<const uint8_t *>(htabs + st.get(sl)) + k * 1024 + lane * 16;
+      __builtin_amdgcn_global_load_lds(src, (LDS_AS void *)(tabs + (sl << 13) + k * 1024), 16, 0, 0);
+    } else {
+      static_assert(kL2Bytes == 512, "two slots' l2 parts per KB chunk");
+      const int sl = 2 * (c - nlc) + (lane >> 5);
+      if (sl < ns) {
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(htabs + st.get(sl)) + kLcBytes + (lane & 31) * 16;
+        __builtin_amdgcn_global_load_lds(src, (LDS_AS void *)(tabs + (ns << 13) + 2 * (c - nlc) * kL2Bytes), 16, 0,
+                                         0);
+      }
+    }
+  }
+}
+
 // At most 80 VGPRs (6 waves per SIMD's worth): the decoder's 16 waves then
 // hold 4 x 80 of a SIMD's 512 registers, and two waves of k_idct (82) from
 // the other batches in flight fit beside them instead of one. k_idct uses no
 // LDS, so it shares the CU without slowing the decoder's LDS-bound rounds
 // (the resize does not: DESIGN.md §4), and the pipeline gains 4-5%
 // (profiles/r5/huff_vgpr_ab_r5h80.txt). The cap costs only SGPR spills to
-// VGPR lanes; at 72 VGPRs scratch spills begin.
+// VGPR lanes; at 72 VGPRs scratch spills begin, and a third k_idct wave per
+// SIMD bought with them (decoder 72 or 64 VGPRs) measured slower
+// (profiles/r5/huff_tabdma_ab_r5dma.txt).
 __global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ data,
@@ -1303,34 +1328,18 @@ __global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_
       if (tid == 0) status[img] = 3;
       return;
     }
-    // the tables' pieces (<= 4 per lane) all in flight before the stream's
-    // first tile, stored once that tile's loads are issued too
-    constexpr int kTabPer = (6 * kTabPieces + kHuffThreads - 1) / kHuffThreads;
-    const int npc = dec.ns * kTabPieces;
-    v4u tv[kTabPer];
-    int tdst[kTabPer];
-#pragma unroll
-    for (int q = 0; q < kTabPer; ++q)
-      tv[q] = *tab_piece_src(htabs, slot_tab, min(tid + q * kHuffThreads, npc - 1), tdst[q], dec.ns);
-    auto store_tabs = [&]() {
-#pragma unroll
-      for (int q = 0; q < kTabPer; ++q)
-        if (tid + q * kHuffThreads < npc) *(LDS_AS v4u *)(tabs + tdst[q]) = tv[q];
-    };
-    if (!destuff_into_window(data, d, (LDS_AS uint8_t *)dyn_lds, sh, tid, status, img, store_tabs)) return;
+    // the tables stream into LDS while the stream's tiles are destuffed
+    stage_tables_dma(htabs, slot_tab, dec.ns, tabs, tid >> 6, tid & 63);
+    if (!destuff_into_window(data, d, (LDS_AS uint8_t *)dyn_lds, sh, tid, status, img)) return;
   } else {
-    // Tables and (when it fits) the whole destuffed stream, byte-swapped, into
-    // LDS, with all of a lane's 16-byte pieces in flight at once (a loop of
-    // single loads waits on each one: ~13 dependent round trips per image).
-    // Every load is unconditional (clamped indices) so that no branch merge
-    // makes the compiler wait for the loads before it.
-    constexpr int kWinPer = 8;
-    const int ns = dec.ns;
-    const int otab = min(tid, kTabPieces - 1);
-    v4u tv[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) // slot q's pieces on lanes 0..kTabPieces-1 (q is uniform)
-      tv[q] = reinterpret_cast<const v4u *>(htabs + slot_tab.get(q < ns ? q : 0))[otab];
+    // Tables (LDS-DMA) and, when it fits, the whole destuffed stream,
+    // byte-swapped, into LDS, a lane's 16-byte pieces kWinPer at a time in
+    // flight. Every load is unconditional (clamped indices) so that no branch
+    // merge makes the compiler wait for the loads before it. (Only images the
+    // fused destuff does not take come here; the four pieces in flight keep
+    // this path's registers below the kernel's cap.)
+    constexpr int kWinPer = 4;
+    stage_tables_dma(htabs, slot_tab, dec.ns, tabs, tid >> 6, tid & 63);
     const v4u *gsrc = reinterpret_cast<const v4u *>(base);
     LDS_AS v4u *wl = (LDS_AS v4u *)dyn_lds;
     const int nwin = in_lds ? (int)(need / 16) : 0;
@@ -1338,15 +1347,6 @@ __global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_
       v4u v[kWinPer];
 #pragma unroll
       for (int k = 0; k < kWinPer; ++k) v[k] = gsrc[max(min(r0 + k * kHuffThreads + tid, nwin - 1), 0)];
-      if (r0 == 0 && tid < kTabPieces) {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          if (q < ns) {
-            const int dst = tid < kLcBytes / 16 ? (q << 13) + 16 * tid : (ns << 13) + q * kL2Bytes + 16 * tid - kLcBytes;
-            *(LDS_AS v4u *)(tabs + dst) = tv[q];
-          }
-        }
-      }
 #pragma unroll
       for (int k = 0; k < kWinPer; ++k) {
         const int i = r0 + k * kHuffThreads + tid;
@@ -1361,6 +1361,7 @@ __global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_
       }
     }
   }
+  __builtin_amdgcn_s_waitcnt(0); // this wave's table DMAs have landed
   __syncthreads();
   const uint64_t t_setup = dbg ? wall_clock64() : 0;
   if (dbg && tid == 0) atomicAdd(dbg + 8, (int)(t_setup - t_start));
