@@ -209,8 +209,10 @@ def main():
     ap.add_argument("--dataset-batches", type=int, default=100,
                     help="batches per rank of one epoch of the dataset legs at N=1 (divided by the world size, at "
                          "least 12, so that the dataset rank 0 writes stays the same size; 0: skip the legs)")
-    ap.add_argument("--dataset-epochs", type=int, default=2,
-                    help="epochs in the dataset leg's timed region (each re-plans, as a training loop does)")
+    ap.add_argument("--dataset-epochs", type=int, default=4,
+                    help="epochs in the dataset leg's timed region (each re-plans, as a training loop does; "
+                         "4 x 100 c2 batches is ~0.17 s: with 2, single host hiccups moved the copying "
+                         "leg by up to 10%% between runs)")
     ap.add_argument("--resize-impl", type=int, default=0,
                     help="LDT_OPT_RESIZE_IMPL of every context (0 auto: k_resize4; 1 its 32-bit 4:2:0 staging; 2 the streaming kernel)")
     ap.add_argument("--resize-waves-pct", type=int, default=0,
