@@ -92,7 +92,8 @@ static int count_step_sim(St *s) {
 }
 static int eq(St a, St b) { return a.p == b.p && a.b == b.b && a.k == b.k; }
 
-typedef struct { St en, ex, cp[2]; int ncp; } Traj;
+typedef struct { St en, ex, cp[16]; int ncp; } Traj;
+static int NCP = 2; /* checkpoints per range (NCP env; the kernel keeps 2: S/3, 2S/3) */
 static long S, nbitsl;
 static int nslot;
 
@@ -100,10 +101,10 @@ static int nslot;
  * prev: stop at the first checkpoint equal to prev's (merge). Returns steps. */
 static int run(int j, St e, const Traj *prev, Traj *out) {
   long stop = (long)(j + 1) * S; if (stop > nbitsl) stop = nbitsl;
-  long c0 = (long)j * S + S / 3, c1 = (long)j * S + (2 * S) / 3;
   St s = e; int steps = 0; out->en = e; out->ncp = 0;
-  long lims[2] = {c0, c1};
-  for (int c = 0; c < 2; c++) {
+  long lims[16];
+  for (int c = 0; c < NCP; c++) lims[c] = (long)j * S + ((c + 1) * S) / (NCP + 1);
+  for (int c = 0; c < NCP; c++) {
     while (s.p < lims[c] && s.p < stop) { step(&s); steps++; }
     if (s.p >= stop) { out->ex = s; return steps; }
     if (prev && prev->ncp > c && eq(prev->cp[c], s)) { out->cp[c] = s; out->ncp = c + 1; out->ex = prev->ex; return steps; }
@@ -128,6 +129,7 @@ int main(int argc, char **argv) {
   for (long q = scan; q < L - 1; q++) { if (d[q] == 0xFF) { if (d[q + 1] == 0) { bits[nbytes++] = 0xFF; q++; continue; } break; } bits[nbytes++] = d[q]; }
   nbitsl = nbytes * 8;
   S = atol(argv[2]);
+  if (getenv("NCP")) NCP = atoi(getenv("NCP"));
   const int spec = atoi(argv[3]);
   const int lanes_cap = argc > 4 ? atoi(argv[4]) : 1024;
   if (S == 0) { S = 256; while ((nbitsl + S - 1) / S > 1024) S += 64; }
