@@ -15,6 +15,8 @@ if os.environ.get("LDT_HUFF_WINDOW"):  # study: cap the LDS stream window (bytes
     ctx.set_option(_lib.OPT_HUFF_WINDOW, int(os.environ["LDT_HUFF_WINDOW"]))
 if os.environ.get("LDT_RESIZE_WG"):  # study: waves per k_resize4 workgroup
     ctx.set_option(_lib.OPT_RESIZE_WG_WAVES, int(os.environ["LDT_RESIZE_WG"]))
+if os.environ.get("LDT_RESIZE_PCT"):  # study: resize bands (LDT_OPT_RESIZE_WAVES_PCT)
+    ctx.set_option(_lib.OPT_RESIZE_WAVES_PCT, int(os.environ["LDT_RESIZE_PCT"]))
 names = ["redo", "wgs", "rounds_sum", "rounds_max", "memo_hits", "write_syms", "write_wave_max", "fallbacks",
          "t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "need_lanes", "need_waves", "t_dc_idct"]
 want = sys.argv[1:] or ["c2", "c1", "c4"]
