@@ -429,6 +429,36 @@ def test_resize_impls_agree_and_coefficients_stay_clean(manifest):
         _check(img[k], oracle.jpeg_to_tensor(nxt[k]), f"after-error[{k}]")
 
 
+def test_resize_band_counts_agree(manifest):
+    """LDT_OPT_RESIZE_WAVES_PCT changes only the band geometry (output rows
+    per wave, and the source rows neighbouring bands both stage): 6 to 36
+    bands per image give identical tensors on the golden images, a c2/c1-shaped
+    batch and raw cells."""
+    import torch
+
+    import ldt_amd
+    from ldt_amd import _lib, synth
+
+    ctx = _lib.get_context(0)
+    cells = [read_golden(e["file"]) for e in manifest["images"]]
+    mixed = synth.q90_512(6, seed=8)[0] + synth.food101_like(10, seed=9)[0]
+    raw = torch.from_numpy(synth.raw_hwc(5, 333, 250, seed=3)).cuda()
+    res = {}
+    try:
+        for pct in (100, 50, 67, 150, 300):
+            ctx.set_option(_lib.OPT_RESIZE_WAVES_PCT, pct)
+            res[pct] = (ldt_amd.decode_tensor_image(_batch(cells))["image"].cpu().numpy(),
+                        ldt_amd.decode_tensor_image(_batch(mixed))["image"].cpu().numpy(),
+                        ldt_amd.resize_raw(raw, 333, 250, normalize=True).cpu().numpy())
+    finally:
+        ctx.set_option(_lib.OPT_RESIZE_WAVES_PCT, 100)  # the default
+    for pct in (50, 67, 150, 300):
+        for k in range(3):
+            assert np.array_equal(res[100][k], res[pct][k]), (pct, k)
+    for k in (0, 7):
+        _check(res[100][1][k], oracle.jpeg_to_tensor(mixed[k]), f"mixed[{k}]")
+
+
 def test_pipelined_to_tensor_fn_host_batches():
     """make_to_tensor_fn: host RecordBatches (as LanceDataset yields them)
     decoded 3 in flight; results match the oracle in order, and a bad row is
