@@ -143,72 +143,48 @@ __device__ __forceinline__ void bytes6(uint32_t w, int lane, int rc, int s[6]) {
 }
 
 // ---- packed 16-bit fancy upsampling (SRC 5) ----
-// A chroma row dword w holds the lane's 4 samples (columns 4*lane..+3); the
-// upsampling context s[0..5] is columns 4*lane-1 .. 4*lane+4, with bytes6's
-// edge rules (column -1 -> column 0, columns past the last one -> the last).
-// Pairs (s[i], s[i+1]) are built as u16x2 by v_perm_b32 from the previous
-// lane's dword, w and the next lane's dword, with per-lane byte selectors
-// that encode the edge rules once (0x0C selects a zero byte).
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-struct Pk5 {
-  u16x2 x01, x12, x23, x34, x45;
-};
-
-__device__ __forceinline__ void pk_selectors(int lane, int rc, uint32_t sel[5]) {
-  int src[6];
-  src[0] = lane == 0 ? 0 : 7; // previous lane's byte 3 (S0 = prev)
-#pragma unroll
-  for (int i = 1; i <= 4; ++i) src[i] = min(i, rc) - 1;
-  src[5] = rc == 5 ? 4 : rc - 1; // next lane's byte 0 (S0 = next)
-#pragma unroll
-  for (int i = 0; i < 5; ++i)
-    sel[i] = (uint32_t)src[i] | (0x0Cu << 8) | ((uint32_t)src[i + 1] << 16) | (0x0Cu << 24);
-}
 
 __device__ __forceinline__ u16x2 as_pk(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 
-__device__ __forceinline__ Pk5 pairs5(uint32_t w, const uint32_t sel[5]) {
-  const uint32_t p = from_prev_lane(w), n = from_next_lane(w);
-  Pk5 r;
-  r.x01 = as_pk(__builtin_amdgcn_perm(p, w, sel[0]));
-  r.x12 = as_pk(__builtin_amdgcn_perm(n, w, sel[1]));
-  r.x23 = as_pk(__builtin_amdgcn_perm(n, w, sel[2]));
-  r.x34 = as_pk(__builtin_amdgcn_perm(n, w, sel[3]));
-  r.x45 = as_pk(__builtin_amdgcn_perm(n, w, sel[4]));
+// A chroma row's upsampling context, columns 4*lane-1 .. 4*lane+4 (jdsample.c
+// edge rules: column -1 -> column 0, columns past the last one -> the last),
+// as six (cb, cr) u16x2 pairs built by v_perm_b32 from the Cb and Cr dwords
+// (4 samples each) and the neighbouring lanes', with per-lane byte selectors
+// that encode the edge rules once (0x0C selects a zero byte). The fancy
+// upsampling's packed 16-bit arithmetic then covers both components at once,
+// and each output pixel's (cb, cr) arrives in one register (round 5: 377 ->
+// 348 VALU per staged row pair against one component per register,
+// standalone c2 resize 0.149 -> 0.146 ms, profiles/r5/resize_cc_r5.txt). Selectors per lane: q[i]
+// for i = 1..4 from (M_hi, M_lo) (own samples, clamped to the last valid
+// column), q[0] from (previous lane's M_hi, M_lo) (lane 0: its own column 0),
+// q[5] from (next lane's M_lo, M_lo or M_hi) (the last valid lane: its own
+// last column).
+struct CC6 {
+  u16x2 q[6];
+};
+
+__device__ __forceinline__ void cc_selectors(int lane, int rc, uint32_t sel[6], bool &x_lo) {
+  auto pair = [](uint32_t b) { return b | (0x0Cu << 8) | ((b + 1u) << 16) | (0x0Cu << 24); };
+  sel[0] = lane == 0 ? pair(0u) : pair(6u);
+#pragma unroll
+  for (int i = 1; i <= 4; ++i) sel[i] = pair(2u * (uint32_t)(min(i, rc) - 1));
+  // q[5]: next lane's column 0 (bytes 4, 5 of (Mn, X)), or own column rc - 1
+  // in X = M_lo (rc <= 2) or M_hi
+  x_lo = rc <= 2;
+  sel[5] = rc == 5 ? pair(4u) : pair(2u * (uint32_t)((rc - 1) & 1));
+}
+
+__device__ __forceinline__ CC6 cc_pairs(uint32_t cbw, uint32_t crw, const uint32_t sel[6], bool x_lo) {
+  const uint32_t mlo = __builtin_amdgcn_perm(crw, cbw, 0x05010400u); // cb0 cr0 cb1 cr1
+  const uint32_t mhi = __builtin_amdgcn_perm(crw, cbw, 0x07030602u); // cb2 cr2 cb3 cr3
+  const uint32_t mp = from_prev_lane(mhi), mn = from_next_lane(mlo);
+  CC6 r;
+  r.q[0] = as_pk(__builtin_amdgcn_perm(mp, mlo, sel[0]));
+#pragma unroll
+  for (int i = 1; i <= 4; ++i) r.q[i] = as_pk(__builtin_amdgcn_perm(mhi, mlo, sel[i]));
+  r.q[5] = as_pk(__builtin_amdgcn_perm(mn, x_lo ? mlo : mhi, sel[5]));
   return r;
-}
-
-// One output row of h2v2_fancy_upsample from the nearer chroma row A and the
-// farther one F: T = 3A + F (vertical), then out[j] = (3T[ci] + T[ci -+ 1] +
-// 8 - (j & 1)) >> 4, ci = j/2 + 1. ev[m] = (out[4m], out[4m+2]),
-// od[m] = (out[4m+1], out[4m+3]). Every value stays below 2^12.
-__device__ __forceinline__ void fancy_pk(const Pk5 &A, const Pk5 &F, u16x2 ev[2], u16x2 od[2]) {
-  const u16x2 three = {3, 3};
-  const u16x2 T01 = A.x01 * three + F.x01, T12 = A.x12 * three + F.x12, T23 = A.x23 * three + F.x23,
-              T34 = A.x34 * three + F.x34, T45 = A.x45 * three + F.x45;
-  const u16x2 c8 = {8, 8}, c7 = {7, 7};
-  ev[0] = (T12 * three + T01 + c8) >> 4;
-  ev[1] = (T34 * three + T23 + c8) >> 4;
-  od[0] = (T12 * three + T23 + c7) >> 4;
-  od[1] = (T34 * three + T45 + c7) >> 4;
-}
-
-// jdcolor.c ycc_rgb_convert for the planar staging (SRC 5): each channel's
-// value before the >> 16, with Y << 16 and the -128 offsets folded in (the
-// same integers: y + ((91881 (cr - 128) + 32768) >> 16) = (Y16 + 91881 cr +
-// 32768 - 91881 * 128) >> 16, an arithmetic shift), clamped to [0, 2^24):
-// byte 2 is the clamped channel value. Luma byte `jb` of the dword yw.
-__device__ __forceinline__ void ycc_x(uint32_t yw, int jb, int cb, int cr, uint32_t &xr, uint32_t &xg,
-                                      uint32_t &xb) {
-  // Y << 16: luma byte jb moved to byte 2 (0x0C selects zero bytes)
-  const int y16 = (int)__builtin_amdgcn_perm(0u, yw, 0x0C000C0Cu | ((uint32_t)jb << 16));
-  const int r = __mul24(91881, cr) + (y16 + (32768 - 91881 * 128));
-  const int g = __mul24(-22554, cb) + __mul24(-46802, cr) + (y16 + (32768 + (22554 + 46802) * 128));
-  const int b = __mul24(116130, cb) + (y16 + (32768 - 116130 * 128));
-  xr = (uint32_t)min(max(r, 0), 0xFFFFFF);
-  xg = (uint32_t)min(max(g, 0), 0xFFFFFF);
-  xb = (uint32_t)min(max(b, 0), 0xFFFFFF);
 }
 
 
@@ -348,7 +324,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
 
   // JPEG fast path: 4:2:0 with both chroma planes fancy-upsampled, W <= 512
   constexpr bool fast420 = SRC == 0 || SRC == 5;
-  constexpr bool kPk = SRC == 5; // packed 16-bit fancy upsampling
+  constexpr bool kPk = SRC == 5; // packed 16-bit fancy upsampling, (cb, cr) pairs
   int rc = 5, cdh = 1;
   // plane geometry copied to registers once: the wave fences in process()
   // would otherwise make every fetch reload it (a dependent global round trip
@@ -357,7 +333,8 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
   int ps0 = 0, ps1 = 0;
   const ImgDesc *dp = nullptr;
   const uint8_t *raw_cell = nullptr;
-  uint32_t psel[5] = {0u, 0u, 0u, 0u, 0u};
+  uint32_t csel[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+  bool cx_lo = false;
   constexpr bool raw_al16 = SRC == 1;
   if constexpr (kJpeg) {
     dp = descs + img;
@@ -365,7 +342,7 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
     const int dw = d.cdw[1];
     rc = lane == (dw - 1) / 4 ? (dw - 1) % 4 + 1 : 5;
     cdh = d.cdh[1];
-    if constexpr (kPk) pk_selectors(lane, rc, psel);
+    if constexpr (kPk) cc_selectors(lane, rc, csel, cx_lo);
     po0 = d.plane_off[0];
     po1 = d.plane_off[1];
     po2 = d.plane_off[2];
@@ -417,29 +394,40 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
     if constexpr (kJpeg) {
       const ImgDesc &d = *dp;
       if constexpr (kPk) {
-        // the same h2v2 fancy upsampling on packed 16-bit pairs: both output
-        // rows' 8 chroma samples of a component in 4 packed registers each
+        // h2v2 fancy upsampling on (cb, cr) pairs, then jdcolor.c
+        // ycc_rgb_convert with the pair in one register: each channel's value
+        // before the >> 16, with Y << 16 and the -128 offsets folded into
+        // constants (y + ((91881 (cr - 128) + 32768) >> 16) = (Y16 + 91881 cr
+        // + 32768 - 91881 * 128) >> 16, an arithmetic shift), clamped to
+        // [0, 2^24) so that byte 2 is the channel; G's two chroma products by
+        // one v_dot2_u32_u16
         const int x0 = lane * 8;
-        u16x2 ev[2][2][2], od[2][2][2]; // [comp][row][pair]
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const Pk5 A = pairs5(jp.c[c][1], psel), U = pairs5(jp.c[c][0], psel),
-                    D = pairs5(jp.c[c][2], psel);
-          fancy_pk(A, U, ev[c][0], od[c][0]);
-          fancy_pk(A, D, ev[c][1], od[c][1]);
-        }
+        const CC6 U = cc_pairs(jp.c[0][0], jp.c[1][0], csel, cx_lo);
+        const CC6 A = cc_pairs(jp.c[0][1], jp.c[1][1], csel, cx_lo);
+        const CC6 D = cc_pairs(jp.c[0][2], jp.c[1][2], csel, cx_lo);
+        const u16x2 three = {3, 3}, c8 = {8, 8}, c7 = {7, 7};
+        const u16x2 wg = {22554, 46802};
+        constexpr uint32_t kKg = 32768u + (22554u + 46802u) * 128u;
+        constexpr int32_t kKr = 32768 - 91881 * 128 - (int32_t)kKg, kKb = 32768 - 116130 * 128 - (int32_t)kKg;
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
+          const CC6 &F = r ? D : U;
+          u16x2 T[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) T[i] = A.q[i] * three + F.q[i];
           uint32_t px[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
+            const int k = j >> 1;
+            const u16x2 P = (j & 1) ? (T[k + 1] * three + T[k + 2] + c7) >> 4 : (T[k + 1] * three + T[k] + c8) >> 4;
+            const uint32_t pw = __builtin_bit_cast(uint32_t, P);
             const uint32_t yw = r ? (j < 4 ? jp.y1.x : jp.y1.y) : (j < 4 ? jp.y0.x : jp.y0.y);
-            // sample j: even j from ev, odd from od; pair j >> 2, half (j >> 1) & 1
-            const int pr = j >> 2, hf = (j >> 1) & 1;
-            const u16x2 cb = (j & 1) ? od[0][r][pr] : ev[0][r][pr], cr = (j & 1) ? od[1][r][pr] : ev[1][r][pr];
-            uint32_t xr, xg, xb;
-            ycc_x(yw, j & 3, hf ? cb.y : cb.x, hf ? cr.y : cr.x, xr, xg, xb);
-            // RGBx: bytes 2 of xr, xg, xb
+            const uint32_t yk = __builtin_amdgcn_perm(0u, yw, 0x0C000C0Cu | ((uint32_t)(j & 3) << 16)) + kKg;
+            const int rr = (int)(yk + __umul24(pw >> 16, 91881u) + (uint32_t)kKr);
+            const int gg = (int)(yk - __builtin_amdgcn_udot2(P, wg, 0u, false));
+            const int bb = (int)(yk + __umul24((uint32_t)(uint16_t)pw, 116130u) + (uint32_t)kKb);
+            const uint32_t xr = (uint32_t)min(max(rr, 0), 0xFFFFFF), xg = (uint32_t)min(max(gg, 0), 0xFFFFFF),
+                           xb = (uint32_t)min(max(bb, 0), 0xFFFFFF);
             px[j] = __builtin_amdgcn_perm(xb, __builtin_amdgcn_perm(xg, xr, 0x0C0C0602u), 0x0C060100u);
           }
           if (x0 < W) {
@@ -448,7 +436,6 @@ __device__ __forceinline__ void resize4_body(const ImgDesc *__restrict__ descs,
             dq[1] = make_uint4(px[4], px[5], px[6], px[7]);
           }
         }
-        (void)d;
       } else if constexpr (fast420) {
         const int x0 = lane * 8;
         int cb[2][8], crr[2][8];
