@@ -21,8 +21,10 @@ Three legs of the same workload, each timed between barriers (max over ranks):
   value_dataset     the reference's iterable loop: an Arrow/Lance dataset of the
                     workload's cells read through LanceDataset + the sampler
                     (ShardedBatchSampler; ShardedFragmentSampler(pad=True) with
-                    its RCCL all_reduce(MAX) for c4 = configs[3]) + to_tensor_fn,
-                    one full epoch (plan included) per rank.
+                    its RCCL all_reduce(MAX) for c4 = configs[3]) + the copying
+                    to_tensor_fn (pylance yields fresh buffers per read), full
+                    epochs (plan included) per rank; value_dataset_registered:
+                    the same with the mapped fragments page-locked in place.
 Each is whole-job (all ranks) with a *_per_gpu twin. Rank 0 prints ONE JSON
 line. The CPU baseline (rank 0, N=1 only) times the reference's own CPU path
 on this host in this run: the map-style DataLoader harness with the PIL
@@ -239,9 +241,12 @@ def main():
                     help="back-to-back runs of the copying host-input leg (value_host_input = their median)")
     ap.add_argument("--dataset-depth", type=int, default=None,
                     help="batches in flight of the dataset legs (default: --depth; 0: make_to_tensor_fn's own choice)")
-    ap.add_argument("--dataset-copy", action="store_true",
-                    help="dataset legs through the copying to_tensor_fn instead of registering the mapped "
-                         "fragments' image buffers")
+    ap.add_argument("--dataset-register", action="store_true",
+                    help="config legs (c3, c4) with the mapped fragments' image buffers page-locked in place "
+                         "(register=True) instead of the copying to_tensor_fn (pylance hands to_tensor_fn a "
+                         "fresh RecordBatch per read, lance_iterable.py:38-41, so copying is the realistic case)")
+    ap.add_argument("--no-dataset-registered", action="store_true",
+                    help="skip the registered-fragment dataset leg (value_dataset_registered)")
     ap.add_argument("--no-workload-legs", action="store_true",
                     help="skip the configs[4] (c5) and progressive (c2p) legs of a c2 run")
     args = ap.parse_args()
@@ -457,18 +462,19 @@ def main():
         else:
             host_ranks = [mine]
 
-    value_dataset = value_dataset_copy = None
-    dataset_info = dataset_copy_info = None
+    value_dataset = value_dataset_reg = None
+    dataset_info = dataset_reg_info = None
     if args.workload != "c5" and args.dataset_batches > 0:
+        # pylance hands to_tensor_fn a fresh RecordBatch per read
+        # (lance_iterable.py:38-41, :53-59): value_dataset is the copying
+        # to_tensor_fn at its own depth; the registered-fragment variant
+        # (register=True, mapped image buffers page-locked once) beside it
         value_dataset, dataset_info = dataset_rate(args, wl, B, world, rank, dev, cells_all, labels_all,
-                                                   barrier, max_over_ranks, keep=not args.dataset_copy)
-        if not args.dataset_copy:
-            # pylance hands to_tensor_fn a fresh RecordBatch per read
-            # (lance_iterable.py:38-41, :53-59): the copying to_tensor_fn at its
-            # own depth, as a loop that cannot register its buffers runs it
-            value_dataset_copy, dataset_copy_info = dataset_rate(args, wl, B, world, rank, dev, cells_all,
-                                                                 labels_all, barrier, max_over_ranks,
-                                                                 copy=True)
+                                                   barrier, max_over_ranks, copy=True,
+                                                   keep=not args.no_dataset_registered)
+        if not args.no_dataset_registered:
+            value_dataset_reg, dataset_reg_info = dataset_rate(args, wl, B, world, rank, dev, cells_all,
+                                                               labels_all, barrier, max_over_ranks, copy=False)
     # BASELINE configs[2] (c3) and configs[3] (c4) as written — the reference's
     # iterable loop over FOOD101-shaped / ImageNet-shaped cells with its own
     # sampler — in the same run as the headline, so that every N of a scaling
@@ -586,10 +592,10 @@ def main():
         res["value_dataset"] = round(value_dataset, 1)
         res["value_dataset_per_gpu"] = round(value_dataset / world, 1)
         res["dataset_leg"] = dataset_info
-    if value_dataset_copy is not None:
-        res["value_dataset_copy"] = round(value_dataset_copy, 1)
-        res["value_dataset_copy_per_gpu"] = round(value_dataset_copy / world, 1)
-        res["dataset_copy_leg"] = dataset_copy_info
+    if value_dataset_reg is not None:
+        res["value_dataset_registered"] = round(value_dataset_reg, 1)
+        res["value_dataset_registered_per_gpu"] = round(value_dataset_reg / world, 1)
+        res["dataset_registered_leg"] = dataset_reg_info
     if workload_legs:
         res["workload_legs"] = workload_legs
     if standalone is not None:
@@ -616,6 +622,7 @@ def main():
         res["decode_efficiency"] = dec
     if args.workload != "c5":
         res["config"]["compressed_bytes_per_img"] = round(comp_bytes, 1)
+    res["profiles_build"] = {"csrc_sha16": csrc_digest(), "refused_stale": STALE}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "c5":
         host_cpus = len(os.sched_getaffinity(0))
         workers = sorted({host_cpus if x == "all" else int(x) for x in args.cpu_workers.split(",") if x}) or None
@@ -628,6 +635,22 @@ def main():
     elif rank == 0 and world == 1 and args.workload == "c5" and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_raw(raw[:8].cpu().numpy())
         res["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 2)
+    # the headline figures once more at the end of the line, after the long
+    # cpu_baseline / workload_legs blobs, so that a tail of the output keeps them
+    summary = {k: res[k] for k in ("value", "value_host_input", "value_host_registered", "value_dataset",
+                                   "value_dataset_registered") if k in res}
+    if config_legs:
+        summary.update({f"config_legs.{k}": v["value"] for k, v in config_legs.items()})
+    for k, v in workload_legs.items():
+        summary[f"workload_legs.{k}"] = v["value"]
+        if "value_host_input" in v:
+            summary[f"workload_legs.{k}.host_input"] = v["value_host_input"]
+    if "gpu_over_cpu" in res:
+        summary["gpu_over_cpu"] = res["gpu_over_cpu"]
+    summary["roofline.frac"] = res["roofline"]["frac"]
+    if "standalone" in res["roofline"]:
+        summary["roofline.standalone.frac"] = res["roofline"]["standalone"]["frac"]
+    res["summary"] = summary
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -644,10 +667,11 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     dataset (the workload's cells repeated to `dataset_batches` batches per
     rank) into fragments of the config's shape; every rank then runs one
     untimed epoch and the timed ones. Padding batches (pad=True) are decoded
-    and counted. `copy` (default --dataset-copy): the copying to_tensor_fn at
-    make_to_tensor_fn's own depth instead of registered fragments at
+    and counted. `copy` (default: not --dataset-register): the copying
+    to_tensor_fn at make_to_tensor_fn's own depth, else registered fragments at
     --dataset-depth. `keep`: leave the dataset for the next leg over the same
-    cells (it is then not written again). Returns (whole-job img/s, info)."""
+    cells (it is then not written again; an exception removes it). Returns
+    (whole-job img/s, info)."""
     import shutil
 
     import numpy as np
@@ -656,7 +680,7 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     import ldt_amd
     from ldt_amd import _lib
 
-    copy = args.dataset_copy if copy is None else copy
+    copy = not args.dataset_register if copy is None else copy
     # the dataset rank 0 writes holds every rank's rows: per-rank batches
     # shrink with the world size (at least 12, or the whole request when that
     # is smaller) so that it stays ~1.7 GB at c2
@@ -676,16 +700,40 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
     rows = sum(sizes)
     import tempfile
 
+    # the path names every size the dataset depends on; a directory left by an
+    # interrupted run is reused only when its row count matches
     path = os.path.join(tempfile.gettempdir(),
-                        f"ldt_bench_ds_{os.environ.get('MASTER_PORT', '0')}_{tag or args.workload}_{world}")
-    if rank == 0 and not os.path.isdir(path):
-        n = len(cells)
-        idx = np.arange(rows) % n
-        tbl = pa.table({"image": pa.array([cells[i] for i in idx], pa.binary()),
-                        "label": pa.array(np.asarray(labels, np.int64)[idx])})
-        ldt_amd.write_dataset(tbl, path, max_rows_per_file=F)
-        del tbl
+                        f"ldt_bench_ds_{os.environ.get('MASTER_PORT', '0')}_{tag or args.workload}_{world}"
+                        f"_n{len(cells)}_b{B}_f{F}_r{rows}")
+    if rank == 0:
+        if os.path.isdir(path):
+            try:
+                ok = ldt_amd.dataset(path).count_rows() == rows
+            except Exception:
+                ok = False
+            if not ok:
+                shutil.rmtree(path, ignore_errors=True)
+        if not os.path.isdir(path):
+            n = len(cells)
+            idx = np.arange(rows) % n
+            tbl = pa.table({"image": pa.array([cells[i] for i in idx], pa.binary()),
+                            "label": pa.array(np.asarray(labels, np.int64)[idx])})
+            ldt_amd.write_dataset(tbl, path, max_rows_per_file=F)
+            del tbl
     barrier()
+    try:
+        return _dataset_epochs(args, wl, B, world, rank, dev, path, rows, sizes, nbatch, copy, barrier,
+                               max_over_ranks)
+    finally:
+        if rank == 0 and not keep:
+            shutil.rmtree(path, ignore_errors=True)
+
+
+def _dataset_epochs(args, wl, B, world, rank, dev, path, rows, sizes, nbatch, copy, barrier, max_over_ranks):
+    """dataset_rate's timed part over the dataset at `path`."""
+    import ldt_amd
+    from ldt_amd import _lib
+
     if wl["sampler"] == "fragment":
         sampler = ldt_amd.ShardedFragmentSampler(rank=rank, world_size=world, pad=True)
     else:
@@ -724,8 +772,6 @@ def dataset_rate(args, wl, B, world, rank, dev, cells, labels, barrier, max_over
         dist.all_reduce(tt)
         tot_imgs = int(tt.item())
     barrier()
-    if rank == 0 and not keep:
-        shutil.rmtree(path, ignore_errors=True)
     info = {"sampler": type(sampler).__name__ + ("(pad=True)" if wl["sampler"] == "fragment" else ""),
             "rows": rows, "fragments": sizes if len(sizes) <= 16 else f"{len(sizes)} fragments",
             "target_batches_per_rank": nbatch, "epochs": args.dataset_epochs,
@@ -864,7 +910,7 @@ def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     return leg
 
 
-PROFILE_ROUND = "r5"  # committed PMC summaries: this round's, else the newest earlier one
+PROFILE_ROUND = "r6"  # committed PMC summaries: this round's, else the newest earlier one
 
 
 def h2d_ceiling(dev, nbytes: int = 256 << 20, reps: int = 5) -> float:
@@ -910,17 +956,47 @@ def stream_copy_ceiling(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
     return best
 
 
+def csrc_digest() -> str:
+    """sha256 (16 hex digits) over the kernel and ABI sources (csrc/*.hip,
+    *.cpp, *.hpp and include/ldt.h): the build a PMC summary was measured on.
+    The tools that write profiles/ summaries record it (tools/traffic_summary.py,
+    tools/decode_eff.py)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    d = os.path.join(REPO, "lance-distributed-training_amd", "csrc")
+    for name in sorted(os.listdir(d)):
+        if name.endswith((".hip", ".cpp", ".hpp")):
+            h.update(name.encode())
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(f.read())
+    with open(os.path.join(REPO, "include", "ldt.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+STALE = []  # committed summaries refused by load_profile (reported in the line)
+
+
 def load_profile(name: str):
     """A committed PMC summary under profiles/<round>/ — this round's, else the
-    newest earlier round's (None if absent); the dict gains its source path."""
+    newest earlier round's — measured on the current kernels: its recorded
+    csrc_sha16 must equal csrc_digest(), so a summary of older kernels (or one
+    without the digest) is refused and listed in STALE. None if absent or
+    stale; the dict gains its source path."""
     rnd = int(PROFILE_ROUND[1:])
+    cur = csrc_digest()
     for r in range(rnd, 0, -1):
         path = os.path.join(REPO, "profiles", f"r{r}", name)
         if os.path.exists(path):
             with open(path) as f:
                 d = json.load(f)
-            if isinstance(d, dict):
-                d.setdefault("source", os.path.relpath(path, REPO))
+            rel = os.path.relpath(path, REPO)
+            if not isinstance(d, dict) or d.get("csrc_sha16") != cur:
+                STALE.append({"file": rel, "csrc_sha16": d.get("csrc_sha16") if isinstance(d, dict) else None,
+                              "current": cur})
+                return None
+            d.setdefault("source", rel)
             return d
     return None
 

@@ -237,6 +237,16 @@ int ldt_host_times(ldt_ctx *ctx, double *us_out, int64_t *calls_out, int reset);
  * CPUs from sysfs, "" if unknown). Creates the pool if needed. */
 int ldt_host_info(ldt_ctx *ctx, char *buf, size_t len);
 
+/* Diagnostics (LDT_OPT_DEBUG_COUNTERS = 1): waits for `stream`, then copies the
+ * parallel Huffman decoder's 16 int32 counters of the last batch into out16,
+ * summed over its images: [1] images, [2] convergence rounds (sum), [3] rounds
+ * (max), [4] memo adoptions, [5] write-pass symbols (sum over lanes), [6] the
+ * symbols of each wave's slowest lane (sum), [8] setup, [9] phase 1, [10]
+ * rounds, [11] block-count scan, [12] write pass (10 ns ticks), [13] needy
+ * slots and [14] the waves they ran on (summed over rounds); [0], [7], [15]
+ * unused. LDT_ERR_ARG when no batch was decoded with the option on. */
+int ldt_debug_counters(ldt_ctx *ctx, int32_t *out16, void *stream);
+
 /* Config 5: raw uint8 HWC cells (no JPEG) -> Resize(224,224) [+Normalize] ->
  * float32 [n,3,224,224]. `hwc` is a device pointer when hwc_is_device != 0,
  * else host (copied through the pinned ring). Cell i starts at

@@ -140,6 +140,7 @@ struct ldt_ctx {
   int64_t stage_cnt[LDT_NUM_STAGES] = {0, 0, 0, 0, 0};
   EvSet *cur_ev = nullptr;
   int64_t last_off_redo = -1; // debug counters of the last batch (plan blob offset)
+  int last_resize_wpg = -1;   // k_resize4 waves per workgroup of the last JPEG batch (0: streaming kernel)
   uint8_t *last_plan_dev = nullptr; // that batch's plan blob on the device
   double host_us[kHpCount] = {};
   int64_t host_calls = 0;
@@ -1018,8 +1019,10 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   {
     // k_resize4 writes the failed images itself; the streaming fallback does not
     hipError_t rerr = hipSuccess;
+    int wpg = 0;
     const bool r4 = c->resize_impl != 2 &&
-                    launch_resize4_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr);
+                    launch_resize4_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s, &rerr, &wpg);
+    c->last_resize_wpg = r4 ? wpg : 0;
     if (!r4) rerr = launch_resize_jpeg(p, w, out_img, labels ? out_lbl : nullptr, s);
     HIPCHK(c, rerr);
     if (!r4) HIPCHK(c, launch_fill_failed(p, w, out_img, labels ? out_lbl : nullptr, s));
@@ -1499,9 +1502,16 @@ int ldt_distributed_indices(ldt_ctx *c, int64_t dataset_len, int num_replicas, i
   return LDT_OK;
 }
 
-// Debug hook: the parallel Huffman decoder's counters of the last batch
-// (redo, workgroups, rounds sum, rounds max, walks, walks converged at the
-// first slot, walk steps, unbounded fallbacks).
+// Debug hook (LDT_OPT_DEBUG_COUNTERS = 1): the parallel Huffman decoder's
+// counters of the last batch, 16 int32 summed over its k_huff_image
+// workgroups (ldt_huffman.hip): [0] unused, [1] workgroups (images), [2]
+// convergence rounds (sum), [3] rounds (max), [4] memo adoptions, [5]
+// write-pass symbols (sum over lanes), [6] write-pass symbols of each wave's
+// slowest lane (sum), [7] unused, [8] setup, [9] phase 1, [10] rounds, [11]
+// block-count scan, [12] write pass + DC scan (10 ns s_memrealtime ticks),
+// [13] needy slots and [14] waves they ran on (summed over rounds), [15]
+// unused. Without the option the kernels get no counter pointer and this
+// returns LDT_ERR_ARG.
 int ldt_debug_counters(ldt_ctx *c, int32_t *out16, void *stream) {
   if (!c || !out16) return LDT_ERR_ARG;
   DeviceGuard g(c->device);
@@ -1512,6 +1522,11 @@ int ldt_debug_counters(ldt_ctx *c, int32_t *out16, void *stream) {
                       hipMemcpyDeviceToHost));
   return LDT_OK;
 }
+
+// Test hook (not part of ldt.h's stable surface): which resize kernel the last
+// JPEG batch took: k_resize4's waves per workgroup (1, 2 or 4), 0 for the
+// streaming kernel, -1 before any batch.
+int ldt_debug_last_resize(ldt_ctx *c) { return c ? c->last_resize_wpg : LDT_ERR_ARG; }
 
 // Test hook (not part of ldt.h's stable surface): Pillow resample coefficient
 // tables computed on the device, for parity tests against the oracle.

@@ -113,8 +113,10 @@ hipError_t launch_resize_jpeg(const DevPlan &p, const DevWork &w, float *out, in
 // One-wave-per-band resize (ldt_resize4.hip); false when unsupported (taps
 // > 11, i.e. sources wider than 1120 px, or LDS), then the streaming
 // workgroup kernel (launch_resize_jpeg / launch_resize_raw) is used.
+// *wpg_used: the waves per workgroup the launch took (a tall batch may need
+// fewer than the default to fit the LDS); untouched when it returns false
 bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
-                         hipStream_t s, hipError_t *err);
+                         hipStream_t s, hipError_t *err, int *wpg_used = nullptr);
 bool launch_resize4_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int wd,
                         const float *lut, float *out, hipStream_t s, hipError_t *err);
 hipError_t launch_resize_raw(const uint8_t *hwc, int64_t cell_stride, int n, int h, int w,

@@ -81,9 +81,6 @@ struct PReader {
   uint64_t buf;
   int bits;
   int marker; // 0: none yet; else the marker code reached
-#ifdef LDT_PROG_STATS
-  int n_sym, n_corr, n_fill, n_slow; // diagnostic counts (see k_prog)
-#endif
 };
 
 // The whole wave runs the decoder with identical values; every value read
@@ -105,13 +102,7 @@ __device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int p) 
 // Appends whole bytes while at most 56 bits are buffered. Fast path: the next
 // 8 window bytes hold no 0xFF (no stuffing, no marker) -> one read of three
 // aligned LDS words instead of a dependent read per byte.
-#ifdef LDT_PROG_STATS
-#define PCNT(r, f, v) ((r).f += (v))
-#else
-#define PCNT(r, f, v)
-#endif
 __device__ __forceinline__ void pfill(PReader &r, const ProgLds &L) {
-  PCNT(r, n_fill, 1);
   if (r.marker == 0 && r.pos + 12 <= r.wl) {
     const int o = r.pos - r.wb;
     const uint32_t a = uni(L.win32[o >> 2]), b = uni(L.win32[(o >> 2) + 1]),
@@ -134,7 +125,6 @@ __device__ __forceinline__ void pfill(PReader &r, const ProgLds &L) {
       return;
     }
   }
-  PCNT(r, n_slow, 1);
   while (r.bits <= 56) {
     int c = 0;
     if (r.marker == 0 && r.pos < r.lim) {
@@ -222,7 +212,6 @@ __device__ __forceinline__ RegTab reg_tab(const ProgTab &t, int lane, bool refin
 // bits (the caller has filled it); consumes its code. Branch-free: a ballot
 // of peek16 < lim[l] over the lanes, its lowest lane l, two readlanes.
 __device__ __forceinline__ int sym_reg(PReader &r, const RegTab &t, int corrupt_sym) {
-  PCNT(r, n_sym, 1);
   const uint32_t w = (uint32_t)(r.buf >> 48);
   const uint64_t hit = __builtin_amdgcn_ballot_w64(w < t.lim);
   const int l = (int)__builtin_ctzll(hit); // 1..17 (lane 17 always matches)
@@ -397,7 +386,6 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
         const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(pc, min(q, 63));
         const int stop = (int)(e & 0xFF);
         int nc = (int)(e >> 8) - ccons; // nonzeros passed: one correction bit each
-        PCNT(R, n_corr, nc);
         if (nc > 32 || nc > R.bits) { // rare: long corrections or a low buffer
           while (nc > 32) {
             deposit((uint32_t)pget(R, L, 32), 32);
@@ -476,21 +464,6 @@ __device__ __forceinline__ void wave_sync() {
 
 } // namespace
 
-// Diagnostic build (-DLDT_PROG_STATS): the luma AC chain's time split, summed
-// over images in 10 ns ticks into the plan's debug counters (dbg[jc]: scan jc
-// from start to end; dbg[4 + jc]: waiting for scan jc-1; dbg[8 + jc]: entropy
-// decode; dbg[12..14]: the last scan's Huffman symbols, correction bits and
-// buffer fills; dbg[15]: luma chains). -DLDT_PROG_STATS=2: every chain's
-// scans, dbg[4 * chain + min(jc, 3)] = scan time (chain 0: the DC scans).
-#ifdef LDT_PROG_STATS
-#define PSTAT_T(v) const uint64_t v = wall_clock64()
-#define PSTAT_ADD(i, t0) \
-  if (stat && w0) atomicAdd(dbg + (i), (int)(wall_clock64() - (t0)))
-#else
-#define PSTAT_T(v)
-#define PSTAT_ADD(i, t0)
-#endif
-
 __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restrict__ descs,
                                              const int32_t *__restrict__ prog_img,
                                              const ProgScan *__restrict__ scans,
@@ -498,7 +471,7 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
                                              const uint8_t *__restrict__ data,
                                              int16_t *__restrict__ pcoef,
                                              int16_t *__restrict__ dcv,
-                                             const int32_t *__restrict__ status, int32_t *dbg) {
+                                             const int32_t *__restrict__ status) {
   __shared__ ProgLds Lw[kWaves];
   __shared__ int progress[kMaxProgScans]; // chunks of each chain scan written back
   // chain 0: the DC scans (dcv only); chain 1 + c: component c's AC scans
@@ -538,14 +511,6 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
       if (d.bcomp[b] == c) b0[c] = b;
   }
   const bool w0 = lane == 0; // the lane that stores
-#ifdef LDT_PROG_STATS
-#if LDT_PROG_STATS == 2
-  const bool stat = dbg != nullptr;
-#else
-  const bool stat = dbg != nullptr && chain == 1;
-  if (stat && w0 && wave == 0) atomicAdd(dbg + 15, 1);
-#endif
-#endif
   int nchain = 0; // the chain's scans (the last one publishes no progress)
   for (int si = 0; si < d.prog_count; ++si) {
     const ProgScan &sc = scans[d.prog_first + si];
@@ -561,9 +526,6 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
     const bool piped = chain != 0;
     if (piped && jc % kWaves != wave) continue; // another wave's scan
     const bool wait_prev = piped && jc > 0;
-    PSTAT_T(t_scan0);
-    const int js = min(jc, 3);
-    (void)js;
     wave_sync();
     RegTab rt = {0u, 0, 0u};
     if (dcband) {
@@ -609,9 +571,6 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
     R.buf = 0;
     R.bits = 0;
     R.marker = 0;
-#ifdef LDT_PROG_STATS
-    R.n_sym = R.n_corr = R.n_fill = R.n_slow = 0;
-#endif
     int pred[4] = {0, 0, 0, 0};
     int eobrun = 0;
     int togo = sc.restart;
@@ -619,13 +578,9 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
     for (int64_t u0 = 0, ci = 0; u0 < units; u0 += upc, ++ci) {
       const int nu = (int)min((int64_t)upc, units - u0);
       const int nbk = nu * bpu;
-      PSTAT_T(t_w0);
       if (wait_prev) // scan jc-1 has written this chunk back
         while (__hip_atomic_load(&progress[jc - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= ci)
           __builtin_amdgcn_s_sleep(1);
-#if LDT_PROG_STATS != 2
-      PSTAT_ADD(4 + js, t_w0);
-#endif
       // stage the chunk's blocks: lane j -> block j of the chunk, scan order
       uint64_t nzv = 0; // lane j: block j's nonzero positions (AC scans)
       if (lane < nbk) {
@@ -668,7 +623,6 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
       }
       wave_sync();
 
-      PSTAT_T(t_dec0);
       uint64_t corr_v = 0, newm_v = 0, negm_v = 0;
       R.wb = (int)uni((uint32_t)L.win_base);
       R.wl = (int)uni((uint32_t)L.win_lim);
@@ -703,9 +657,6 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
       }
       if (w0) L.pos = R.pos;
       wave_sync();
-#if LDT_PROG_STATS != 2
-      PSTAT_ADD(8 + js, t_dec0);
-#endif
       if (lane < nbk) {
         const int64_t gb = L.bidx[lane];
         if (!dcband && Ah != 0) { // apply this block's refinement: corrections, then new values
@@ -746,25 +697,13 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
       wave_sync();
 
     }
-#if LDT_PROG_STATS == 2
-    PSTAT_ADD(4 * chain + js, t_scan0);
-#else
-    PSTAT_ADD(js, t_scan0);
-#endif
-#if LDT_PROG_STATS == 1
-    if (stat && w0 && jc == 3) {
-      atomicAdd(dbg + 12, R.n_sym);
-      atomicAdd(dbg + 13, R.n_corr);
-      atomicAdd(dbg + 14, R.n_fill);
-    }
-#endif
   }
 }
 
 hipError_t launch_prog(const DevPlan &p, const DevWork &w, hipStream_t s) {
   if (p.n_prog == 0) return hipSuccess;
   hipLaunchKernelGGL(k_prog, dim3(4 * p.n_prog), dim3(64 * kWaves), 0, s, p.descs, p.prog_img, p.pscans, p.ptabs,
-                     w.data, w.pcoef, w.dcv, w.status, p.redo);
+                     w.data, w.pcoef, w.dcv, w.status);
   return hipGetLastError();
 }
 

@@ -754,13 +754,19 @@ static int waves_target4(const Geom4 &g, int pct, int max_waves = 12) {
 }
 
 bool launch_resize4_jpeg(const DevPlan &p, const DevWork &w, float *out, int64_t *out_labels,
-                         hipStream_t s, hipError_t *err) {
+                         hipStream_t s, hipError_t *err, int *wpg_used) {
   Geom4 g;
   const int ks_h = resample_ksize_host(p.max_w, kOut);
   if (ks_h > 11) return false;
-  const int wpg = p.resize_wpg > 0 ? p.resize_wpg : kResizeWavesJpeg;
-  if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, wpg, true)) return false;
+  // a tall image (large ring) may not fit 4 waves' LDS in one workgroup:
+  // fewer waves per workgroup before giving the batch to the streaming kernel
+  int wpg = p.resize_wpg > 0 ? p.resize_wpg : kResizeWavesJpeg;
+  while (!make_geom4(p.n, p.max_w, p.max_h, ks_h, 1, g, wpg, true)) {
+    if (wpg == 1) return false;
+    wpg >>= 1;
+  }
   if (!make_geom4(p.n, p.max_w, p.max_h, ks_h, waves_target4(g, p.resize_waves_pct), g, wpg, true)) return false;
+  if (wpg_used) *wpg_used = wpg;
   RawSrc raw{nullptr, 0, 0, 0};
   // fast-path images and the rest go to separate kernels (each skips the
   // other's images); a batch of one kind launches one kernel. The first

@@ -72,7 +72,7 @@ EXPORTED = (
     "ldt_decode_batch", "ldt_decode_batch_large", "ldt_decode_batch_resident",
     "ldt_register_host", "ldt_unregister_host", "ldt_fetch_status", "ldt_last_ticket", "ldt_fetch_status_ticket",
     "ldt_stage_times", "ldt_host_times", "ldt_host_info", "ldt_resize_raw", "ldt_shard_ranges",
-    "ldt_shard_fragments", "ldt_distributed_indices",
+    "ldt_shard_fragments", "ldt_distributed_indices", "ldt_debug_counters",
 )
 
 
@@ -150,6 +150,8 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
                                               vp, vp]
         L.ldt_debug_resample_coeffs.argtypes = [vp, i32, i32, vp, vp, vp]
         L.ldt_debug_counters.argtypes = [vp, vp, vp]
+        L.ldt_debug_last_resize.argtypes = [vp]
+        L.ldt_debug_last_resize.restype = ctypes.c_int
         L.ldt_register_host.argtypes = [vp, vp, sz]
         L.ldt_unregister_host.argtypes = [vp, vp]
         for name in ("ldt_set_option", "ldt_set_copy_stream", "ldt_decode_batch", "ldt_decode_batch_large", "ldt_register_host",
@@ -208,6 +210,17 @@ class Context:
         self.check(self.lib.ldt_host_times(self.handle, us.ctypes.data, ctypes.byref(calls), int(reset)),
                    "ldt_host_times")
         return {k: float(us[i]) for i, k in enumerate(HOST_PHASES)}, int(calls.value)
+
+    def debug_counters(self, stream=None):
+        """The parallel Huffman decoder's 16 counters of the last batch
+        (LDT_OPT_DEBUG_COUNTERS = 1; layout in ldt.h), as a list of ints."""
+        import numpy as np
+
+        out = np.zeros(16, np.int32)
+        self.check(self.lib.ldt_debug_counters(self.handle, out.ctypes.data,
+                                               stream.cuda_stream if stream is not None else None),
+                   "ldt_debug_counters")
+        return out.tolist()
 
     def host_info(self) -> dict:
         """The host copy placement (ldt_host_info): copy threads and their

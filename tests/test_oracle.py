@@ -156,3 +156,9 @@ def test_fullbatch_fixture_matches_oracle():
         raw = synth.raw_hwc_one(1024, 1024, g["seed"] * 100003 + i)
         assert hashlib.sha256(oracle.raw_to_tensor(raw, normalize=True).tobytes()).hexdigest() == \
             g["c5"]["sha256"][i]
+    # c3 / c4: the whole 128-image batches (cells and labels regenerate exactly)
+    for key, make in (("c3", synth.food101_like), ("c4", synth.imagenet_like)):
+        cells, labels = make(g[key]["n"], seed=g["seed"])
+        assert [int(x) for x in labels] == g[key]["labels"]
+        got = [hashlib.sha256(oracle.jpeg_to_tensor(b).tobytes()).hexdigest() for b in cells]
+        assert got == g[key]["sha256"], key

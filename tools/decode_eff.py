@@ -7,7 +7,10 @@
                 issuing VALU)
   lds_bank_conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 usage: python tools/decode_eff.py <pmc dir> <workload> > summary.json"""
-import collections, csv, glob, json, sys
+import collections, csv, glob, json, os, sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import csrc_digest  # noqa: E402
 
 d, wl = sys.argv[1], sys.argv[2]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -15,7 +18,7 @@ for f in glob.glob(f"{d}/p*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("ldt::", "")
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-out = {"workload": wl, "source": "rocprofv3 --pmc passes (tools/pmc.sh) over one batch at a time", "kernels": {}}
+out = {"csrc_sha16": csrc_digest(), "workload": wl, "source": "rocprofv3 --pmc passes (tools/pmc.sh) over one batch at a time", "kernels": {}}
 for k, c in sorted(acc.items()):
     m = {n: sum(v) / len(v) for n, v in c.items()}
     if "SQ_INSTS_VALU" not in m or "GRBM_GUI_ACTIVE" not in m:

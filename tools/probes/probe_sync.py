@@ -5,7 +5,9 @@ import torch, ldt_amd
 from ldt_amd import _lib, synth
 ctx = _lib.get_context(0)
 ctx.set_option(_lib.OPT_DEBUG_COUNTERS, 1)
-names = ["redo", "wgs", "rounds_sum", "rounds_max", "walks", "walk_first", "walk_steps", "fallbacks", "boundaries"]
+# ldt_debug_counters layout (ldt_abi.cpp)
+names = ["unused0", "wgs", "rounds_sum", "rounds_max", "memo_hits", "write_syms", "write_wave_max", "unused7",
+         "t_setup", "t_phase1", "t_rounds", "t_scan", "t_write", "need_lanes", "need_waves"]
 for wl, fn, n in (("c2", synth.q90_512, 64), ("c1", synth.food101_like, 64), ("c4", synth.imagenet_like, 64)):
     cells, labels = fn(n, seed=1)
     for S in (512, 1024, 2048):
@@ -14,4 +16,4 @@ for wl, fn, n in (("c2", synth.q90_512, 64), ("c1", synth.food101_like, 64), ("c
         rb.decode()
         out = np.zeros(16, np.int32)
         ctx.check(ctx.lib.ldt_debug_counters(ctx.handle, out.ctypes.data, None), "dbg")
-        print(wl, S, dict(zip(names, out[:9].tolist())), flush=True)
+        print(wl, S, dict(zip(names, out[:15].tolist())), flush=True)

@@ -1,0 +1,105 @@
+"""Does the pipeline's rate survive a DDP-like process?
+
+One process per run (stream-to-queue binding is per process): creates the
+streams a DDP training process would (lance_iterable.py:80,95: the process
+group and DDP before the loop) BEFORE or AFTER building the to_tensor_fn, then
+times the host-input legs of c2 (make_to_tensor_fn(), adaptive) and c2p
+(make_to_tensor_fn(depth=7)) with a comm-like stream the consumer waits on at
+every step (DDP's gradient all-reduce). usage:
+    python tools/probes/stream_env.py clean|before|after [c2|c2p] [steps]
+Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "lance-distributed-training_amd"))
+sys.path.insert(0, REPO)
+
+
+def ddp_env(dev):
+    """Process group (RCCL, world 1, one all_reduce so that its communicator
+    and streams exist), four torch side streams used once, and the comm-like
+    stream returned for the per-step wait."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    t = torch.ones(1 << 20, device=dev)
+    dist.all_reduce(t)
+    side = [torch.cuda.Stream(dev) for _ in range(4)]
+    for s in side:
+        with torch.cuda.stream(s):
+            t.add_(1)
+    comm = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    return comm, side, t
+
+
+def main():
+    mode = sys.argv[1]
+    wl = sys.argv[2] if len(sys.argv) > 2 else "c2"
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 100
+    import numpy as np
+    import pyarrow as pa
+    import torch
+
+    import ldt_amd
+    from bench import make_cells
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    comm = side = buf = None
+    if mode == "before":
+        comm, side, buf = ddp_env(dev)
+    fn = ldt_amd.make_to_tensor_fn(depth=7 if wl == "c2p" else None, device=dev)
+    B = 256
+    cells, labels = make_cells(wl, B, seed=11)
+    host = [pa.RecordBatch.from_arrays([pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
+                                       names=["image", "label"])]
+    cells2, labels2 = make_cells(wl, B, seed=12)
+    host.append(pa.RecordBatch.from_arrays([pa.array(cells2, pa.binary()),
+                                            pa.array(np.asarray(labels2, np.int64))], names=["image", "label"]))
+    fn(host[0])  # first use of the pipeline's streams
+    torch.cuda.synchronize(dev)
+    if mode == "after":
+        comm, side, buf = ddp_env(dev)
+    k = [0]
+
+    def step():
+        out = fn(host[k[0] % 2])
+        k[0] += 1
+        if comm is not None:
+            # DDP-like: the consumer's stream waits for a comm-stream op
+            comm.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(comm):
+                buf.mul_(1.0)
+            torch.cuda.current_stream(dev).wait_stream(comm)
+        return out
+
+    t0 = time.perf_counter()
+    n = 0
+    while n < 60 or time.perf_counter() - t0 < 0.5:
+        step()
+        n += 1
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    fn.check()
+    print(json.dumps({"mode": mode, "workload": wl, "img_s": round(B * steps / dt, 1), "steps": steps,
+                      "slot_priority_env": os.environ.get("LDT_SLOT_PRIORITY"),
+                      "depth": fn.pipeline.depth, "high_priority": fn.pipeline.high_priority}), flush=True)
+    if mode != "clean":
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -5,7 +5,10 @@ FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB per dispatch
 FETCH_SIZE reports exactly half the bytes of wide streaming reads (128-B
 requests tallied at 64 B), so it is doubled; WRITE_SIZE is exact for 16-B
 stores. Printed as JSON; bench.py embeds it as roofline.traffic."""
-import csv, glob, json, sys
+import csv, glob, json, os, sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import csrc_digest  # noqa: E402
 
 d, workload = sys.argv[1], sys.argv[2]
 vals = {}
@@ -26,6 +29,7 @@ except OSError:
 fetch = sum(vals["FETCH_SIZE"]) / max(len(vals["FETCH_SIZE"]), 1) * 1024
 write = sum(vals["WRITE_SIZE"]) / max(len(vals["WRITE_SIZE"]), 1) * 1024
 print(json.dumps({
+    "csrc_sha16": csrc_digest(),
     "workload": workload, "kernel": "k_resize4", "dispatches": [len(vals["FETCH_SIZE"]), len(vals["WRITE_SIZE"])],
     "fetch_size_raw_bytes": round(fetch), "write_size_bytes": round(write),
     "hbm_bytes_per_launch": round(2 * fetch + write),
