@@ -804,7 +804,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   // destuff_into_window); those images get no destuff chunks (ds_count 0)
   int n_ds_img = 0; // baseline images left to k_destuff_*
   {
-    int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs);
+    int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds_image(max_tabs);
     if (c->win_cap >= 0) cap = std::min<int64_t>(cap, c->win_cap);
     const int64_t winb = std::min<int64_t>(max_window, cap) & ~(int64_t)15;
     chunk_img.clear();
@@ -962,7 +962,7 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   {
     // LDS window of k_huff_image: the largest image's stream, capped by what
     // is left of the CU's LDS after the tables (bigger streams read global)
-    int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds(max_tabs);
+    int64_t cap = kHuffLdsMax - kHuffStaticLds - huff_tab_lds_image(max_tabs);
     if (c->win_cap >= 0) cap = std::min<int64_t>(cap, c->win_cap);
     p.win_bytes = (int)(std::min<int64_t>(max_window, cap) & ~(int64_t)15);
   }

@@ -122,6 +122,7 @@ struct Rd {
     wi += m ? 1 : 0;
   }
   __device__ __forceinline__ void refill() { nxt = src(wi); }
+  __device__ __forceinline__ int32_t pos() const { return p; }
 };
 
 // ---------------------------------------------------------------------------
@@ -301,23 +302,25 @@ __device__ __forceinline__ uint32_t lookup(const Dec &dec, const St &st, uint32_
 
 // HUFF_EXTEND of the s magnitude bits following the code.
 // raw < 2^(s-1) (top magnitude bit clear) is negative: raw - (2^s - 1); the
-// s-bit mask is one v_bfm (s = 0: raw = mask = 0, value 0).
+// s-bit mask is one bit-field extract of all ones (s = 0: raw = mask = 0,
+// value 0).
 __device__ __forceinline__ int ext_value(uint32_t pk, uint32_t e) {
   const uint32_t total = e & 31, s = (e >> 5) & 15;
   const int raw = (int)__builtin_amdgcn_ubfe(pk, 32 - total, s);
-  const int mask = (int)((1u << s) - 1u);
+  const int mask = (int)__builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, s);
   return raw <= (mask >> 1) ? raw - mask : raw;
 }
 
 // k += adv; k >= 64 ends the block (EOB advances by 64).
-__device__ __forceinline__ void advance(St &st, const Dec &dec, int adv) {
+__device__ __forceinline__ void advance(St &st, int b3end, int adv) {
   const int k2 = st.k + adv;
   const bool end = k2 >= 64;
   int nb = st.b3 + 3;
-  nb = nb == dec.b3end ? 0 : nb;
+  nb = nb == b3end ? 0 : nb;
   st.b3 = end ? nb : st.b3;
   st.k = end ? 0 : k2;
 }
+__device__ __forceinline__ void advance(St &st, const Dec &dec, int adv) { advance(st, dec.b3end, adv); }
 
 // Count-only step (blocks started) on the count-mode entries (HuffTab.lc
 // high half, see ldt_types.hpp): one lookup consumes a run of AC symbols of
@@ -462,6 +465,173 @@ __device__ __forceinline__ int write_run(Rd<W> &R, St &st, const Dec &dec, int32
     }
     rs.put(base + cursor, gmask | (cursor == 0 ? 256u : 0u) | (dcd << 16));
   }
+  return iters;
+}
+
+// ---------------------------------------------------------------------------
+// k_huff_image's write pass (round 6): the same output as write_run, with the
+// open coefficient group staged in LDS instead of registers.
+//
+// The write pass is bound by VALU issue (16 waves), and with
+// the lanes at different points of their decodes every path of the loop body
+// issues in nearly every iteration. write_run's register group (two 64-bit
+// halves: a 64-bit shift, selects and ORs to place each value, and selects to
+// clear it) and its unit pairing cost ~20 of its ~100 VALU per iteration.
+// Here the lane's open group lives in 8 LDS planes of u16 (slot q of lane t
+// at planes + q * 2048 + 2 t, so a value lands with one ds_write_b16 at an
+// address of 2 VALU); a flush reads the 8 halves back (LDS loads, no VALU),
+// stores the 16-byte unit at once and writes zeros behind it. The l1 lookup
+// reads the compacted tables (compact_tables).
+// ---------------------------------------------------------------------------
+struct DecW {
+  lds_cu8 l1;        // compacted l1 entries: slot s at byte s << 12
+  lds_cu8 l2;        // l2 parts: slot s at byte s * kL2Bytes
+  uint32_t dcseq, acseq;
+  int b3end;
+  const HuffTab *g;
+  const ImgDesc *d;
+};
+
+// The write pass's lookup (l1 entry, as lookup()).
+__device__ __forceinline__ uint32_t lookup_w(const DecW &dec, const St &st, uint32_t pk) {
+  const bool ac = st.k != 0;
+  const uint32_t slot = __builtin_amdgcn_ubfe(ac ? dec.acseq : dec.dcseq, (uint32_t)st.b3, 3u);
+  uint32_t e = *(lds_cu16)(dec.l1 + (slot << 12) + ((pk >> (32 - kLookBits)) << 1));
+  if (__builtin_expect(__any((e & 31) == 0), 0)) {
+    if ((e & 31) == 0) {
+      if (e == kHuffCanon)
+        e = lookup_canon(dec.g, dec.d, st.b3 / 3, ac, pk);
+      else
+        e = ((lds_cu16)(dec.l2 + slot * kL2Bytes))[((e >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
+    }
+  }
+  return e;
+}
+
+// After the rounds (no lane reads the count-mode halves any more): each
+// table's l1 halves become a 4 KB u16 array at slot << 12, its l2 part moves
+// to (ns << 12) + slot * kL2Bytes, and the group planes at ns *
+// kTabCompactBytes (kHuffPlaneBytes, within huff_tab_lds_image) are zeroed.
+// Entries are moved in chunks of 4 per lane in increasing order, each read
+// before a barrier and written after it: entry j moves from byte 4j to 2j, so
+// a chunk's writes stay below every later chunk's sources. Contains
+// __syncthreads (two per chunk).
+__device__ __forceinline__ DecW compact_tables(const Dec &dec, LDS_AS uint8_t *tabs, int tid,
+                                              LDS_AS uint8_t *&planes) {
+  const int ns = dec.ns;
+  const int nw = ns << (kLookBits); // lc words (2048 per table)
+  const int nl2 = ns * (kL2Bytes / 4);
+  const uint32_t l2w = tid < nl2 ? ((lds_cu32)(tabs + (ns << 13)))[tid] : 0u;
+  for (int c0 = 0; c0 < nw; c0 += 4 * kHuffThreads) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = c0 + tid + i * kHuffThreads;
+      w[i] = j < nw ? ((lds_cu32)tabs)[j] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = c0 + tid + i * kHuffThreads;
+      if (j < nw) ((LDS_AS uint16_t *)tabs)[j] = (uint16_t)w[i];
+    }
+    __syncthreads();
+  }
+  // the l2 parts (read above, before any write) below the group planes
+  if (tid < nl2) ((LDS_AS uint32_t *)(tabs + (ns << 12)))[tid] = l2w;
+  planes = tabs + ns * kTabCompactBytes;
+  static_assert(kHuffPlaneBytes == 16 * kHuffThreads, "one 16-byte piece per lane");
+  ((LDS_AS v4u *)planes)[tid] = (v4u)(0u);
+  __syncthreads();
+  DecW dw;
+  dw.l1 = tabs;
+  dw.l2 = tabs + (ns << 12);
+  dw.dcseq = dec.dcseq;
+  dw.acseq = dec.acseq;
+  dw.b3end = dec.b3end;
+  dw.g = dec.g;
+  dw.d = dec.d;
+  return dw;
+}
+
+// write_run with the open group in the lane's LDS planes (lp = planes + 2 *
+// lane, see above): block ownership, records, carries and the packed units
+// exactly as write_run writes them (units one 16-byte store each).
+// The lane's open group as a 16-byte unit: the 8 plane halves loaded as
+// packed pairs (ds_read_u16_d16 / _d16_hi fill a register's halves without
+// VALU).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 plane_unit(const LDS_AS uint16_t *lp) {
+  uint32_t r[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    s16x2 h;
+    h.x = (short)lp[(2 * d) * kHuffThreads];
+    h.y = (short)lp[(2 * d + 1) * kHuffThreads];
+    r[d] = __builtin_bit_cast(uint32_t, h);
+  }
+  return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+template <class RD, class RS>
+__device__ __forceinline__ int write_run_lds(RD &R, St &st, const DecW &dec, int32_t stop,
+                                              int &cursor, int lim, uint4 *__restrict__ coef_img,
+                                              const RS &rs, int base, LDS_AS uint16_t *lp) {
+  int cg = -1;                       // the open group's index; < 0: none
+  uint32_t wu = (uint32_t)base * 8u; // units stored
+  uint32_t gmask = 0;                // groups of the current block
+  uint32_t dcd = 0;                  // its DC difference (16 bits)
+  int bcur = base + cursor;          // image block of the current block (base - 1: none owned yet)
+  const int blast = base + lim - 1;  // the last block the run may own
+  bool go = (R.pos() < stop || st.k != 0) && !(st.k == 0 && bcur >= blast);
+  int iters = 0;
+  while (go) {
+    ++iters;
+    R.refill();
+    const bool first = st.k == 0; // a block starts: its DC symbol
+    const uint32_t pk = R.peek();
+    const uint32_t e = lookup_w(dec, st, pk);
+    const int v = ext_value(pk, e);
+    const int adv = (int)(e >> 9);
+    // a corrupt stream can run k past 63 (a run or ZRL from k > 48): jdhuff.c
+    // then stores into natural[k >= 64] = position 63; so does this clamp.
+    const int slot = min(st.k + adv - 1, 63);
+    const int g = slot >> 3;
+    // a nonzero AC value of an owned block (an AC value is nonzero iff s != 0)
+    const bool put = !first && (e & (15u << 5)) != 0 && bcur >= base;
+    const bool opens = put && g != cg;
+    if (cg >= 0 && (first || opens)) {
+      // the open group is complete: its unit, then zeros behind it
+      const uint4 u = plane_unit(lp);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) lp[q * kHuffThreads] = 0;
+      coef_img[wu] = u;
+      ++wu;
+      gmask |= 1u << cg;
+    }
+    if (put) lp[(slot & 7) * kHuffThreads] = (uint16_t)v;
+    // a block starts: the previous one's record, then this block's state
+    if (first) {
+      if (bcur >= base) rs.put(bcur, gmask | (bcur == base ? 256u : 0u) | (dcd << 16));
+      ++bcur;
+      if ((bcur & 63) == 0) rs.put_carry(bcur >> 6, wu);
+    }
+    gmask = first ? 0u : gmask;
+    dcd = first ? (uint32_t)v & 0xFFFFu : dcd;
+    cg = first ? -1 : (opens ? g : cg);
+    R.consume_nl((int)(e & 31));
+    advance(st, dec.b3end, adv);
+    go = (R.pos() < stop || st.k != 0) && !(st.k == 0 && bcur >= blast);
+  }
+  if (bcur >= base) {
+    if (cg >= 0) {
+      coef_img[wu] = plane_unit(lp);
+      gmask |= 1u << cg;
+      ++wu;
+    }
+    rs.put(bcur, gmask | (bcur == base ? 256u : 0u) | (dcd << 16));
+  }
+  cursor = bcur - base;
   return iters;
 }
 
@@ -1021,6 +1191,11 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   sh.ex_p[tid] = pre;
   __syncthreads();
   const uint64_t t_scan = dbg ? wall_clock64() : 0;
+#ifndef LDT_WRITE_REG
+  // the count-mode halves are dead: compact the tables, zero the group planes
+  LDS_AS uint8_t *planes;
+  const DecW decw = compact_tables(dec, (LDS_AS uint8_t *)dec.tabs, tid, planes);
+#endif
 
   // ---- write pass from the true entry ----
   // block records into LDS (the slot state is dead from here) when they fit
@@ -1040,12 +1215,22 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     R.src = src;
     R.seek(g.pbias + wp);
     uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
+#ifdef LDT_WRITE_REG // A/B: round 5's register-group write pass
     if (rec_lds)
       witers = write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
                          RecLds{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry}, base);
     else
       witers = write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
                          RecGlob{brec + d.coef_off, bcarry + d.coef_off / 64}, base);
+#else
+    LDS_AS uint16_t *lp = (LDS_AS uint16_t *)planes + tid;
+    const RecLds rl{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry};
+    const RecGlob rg{brec + d.coef_off, bcarry + d.coef_off / 64};
+    if (rec_lds)
+      witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rl, base, lp);
+    else
+      witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rg, base, lp);
+#endif
     if (g.j == sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;
@@ -1380,7 +1565,7 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kHuffLdsMax - kHuffStaticLds);
   if (attr != hipSuccess) return attr;
-  const size_t lds = (size_t)p.win_bytes + huff_tab_lds(p.max_tabs);
+  const size_t lds = (size_t)p.win_bytes + huff_tab_lds_image(p.max_tabs);
   hipLaunchKernelGGL(k_huff_image, dim3(p.n_par), dim3(kHuffThreads), lds, s, p.descs, p.segs,
                      p.htabs, w.data, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.brec, w.bcarry,
                      w.status, p.redo);

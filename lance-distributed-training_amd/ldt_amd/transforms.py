@@ -619,7 +619,8 @@ class DecodePipeline:
         # = 0 / 1 forces either.
         n_high, slot_dma = slot_streams(self.depth, _lib.hw_queues(), os.environ.get("LDT_SLOT_PRIORITY"))
         if self.adaptive:
-            n_high, slot_dma = 0, True
+            env = os.environ.get("LDT_SLOT_PRIORITY")
+            n_high, slot_dma = (self.depth if env is not None and int(env) else 0), True
         self.high_priority = n_high > 0
         if slot_dma:
             for c in self.ctxs:

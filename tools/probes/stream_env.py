@@ -55,7 +55,9 @@ def main():
     comm = side = buf = None
     if mode == "before":
         comm, side, buf = ddp_env(dev)
-    fn = ldt_amd.make_to_tensor_fn(depth=7 if wl == "c2p" else None, device=dev)
+    depth = int(os.environ.get("LDT_PROBE_DEPTH", "0")) or (7 if wl == "c2p" else None)
+    fn = ldt_amd.make_to_tensor_fn(depth=depth, device=dev)
+    resident = os.environ.get("LDT_PROBE_RESIDENT") == "1"
     B = 256
     cells, labels = make_cells(wl, B, seed=11)
     host = [pa.RecordBatch.from_arrays([pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
@@ -69,8 +71,10 @@ def main():
         comm, side, buf = ddp_env(dev)
     k = [0]
 
+    rbs = [ldt_amd.ResidentBatch(cells, labels, device=dev), ldt_amd.ResidentBatch(cells2, labels2, device=dev)]
+
     def step():
-        out = fn(host[k[0] % 2])
+        out = fn.pipeline.decode(rbs[k[0] % 2]) if resident else fn(host[k[0] % 2])
         k[0] += 1
         if comm is not None:
             # DDP-like: the consumer's stream waits for a comm-stream op
@@ -94,7 +98,8 @@ def main():
     fn.check()
     print(json.dumps({"mode": mode, "workload": wl, "img_s": round(B * steps / dt, 1), "steps": steps,
                       "slot_priority_env": os.environ.get("LDT_SLOT_PRIORITY"),
-                      "depth": fn.pipeline.depth, "high_priority": fn.pipeline.high_priority}), flush=True)
+                      "depth": fn.pipeline.depth, "high_priority": fn.pipeline.high_priority,
+                      "resident": resident}), flush=True)
     if mode != "clean":
         import torch.distributed as dist
 
