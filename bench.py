@@ -860,8 +860,8 @@ def leg_c5(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
 def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     """The c2 images encoded progressive (SOF2), batch
     256, 7 in flight (DecodePipeline: 4 slots on high-priority streams):
-    `value` with the cells resident, `value_host_input` from a host
-    RecordBatch, both through one make_to_tensor_fn(depth=7)'s pipeline; CPU leg: the
+    `value` with the cells resident (DecodePipeline(depth=7)),
+    `value_host_input` from a host RecordBatch (make_to_tensor_fn(depth=7)); CPU leg: the
     reference map-style DataLoader at this box's CPU share of workers."""
     import numpy as np
     import pyarrow as pa
@@ -873,12 +873,9 @@ def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     B = WORKLOADS["c2p"]["batch"]
     cells, labels = make_cells("c2p", B, seed=1000 * rank)
     rb = ldt_amd.ResidentBatch(cells, labels, device=dev)
-    # one 7-deep pipeline for both legs: the to_tensor_fn's own. A second
-    # pipeline's streams, drawn later from torch's pool after the c2 legs',
-    # put one slot on the consumer's hardware queue (39-41k
-    # host input against 48-49k on the first pipeline's streams)
-    fn = ldt_amd.make_to_tensor_fn(depth=7, device=dev)
-    pipe = fn.pipeline
+    # the resident leg on its own 7-deep pipeline, the host leg on the
+    # to_tensor_fn's (both on the device's shared slot streams)
+    pipe = ldt_amd.DecodePipeline(depth=7, device=dev)
     for c in pipe.ctxs:
         c.set_option(_lib.OPT_PROFILE, 1)
     # ~5 ms per batch 7 deep: at least 60 steps, so that fill and drain stay small
@@ -896,6 +893,7 @@ def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     del pipe
     host = pa.RecordBatch.from_arrays([pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
                                       names=["image", "label"])
+    fn = ldt_amd.make_to_tensor_fn(depth=7, device=dev)
     th = _warm_then_time(lambda: fn(host), K, 15, 0.25, barrier, max_over_ranks)
     fn.check()
     leg["value_host_input"] = round(B * K * world / th, 1)

@@ -1191,11 +1191,9 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   sh.ex_p[tid] = pre;
   __syncthreads();
   const uint64_t t_scan = dbg ? wall_clock64() : 0;
-#ifndef LDT_WRITE_REG
   // the count-mode halves are dead: compact the tables, zero the group planes
   LDS_AS uint8_t *planes;
   const DecW decw = compact_tables(dec, (LDS_AS uint8_t *)dec.tabs, tid, planes);
-#endif
 
   // ---- write pass from the true entry ----
   // block records into LDS (the slot state is dead from here) when they fit
@@ -1215,14 +1213,6 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     R.src = src;
     R.seek(g.pbias + wp);
     uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
-#ifdef LDT_WRITE_REG // A/B: round 5's register-group write pass
-    if (rec_lds)
-      witers = write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
-                         RecLds{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry}, base);
-    else
-      witers = write_run(R, st, dec, wstop, cursor, total - bstart, cimg,
-                         RecGlob{brec + d.coef_off, bcarry + d.coef_off / 64}, base);
-#else
     LDS_AS uint16_t *lp = (LDS_AS uint16_t *)planes + tid;
     const RecLds rl{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry};
     const RecGlob rg{brec + d.coef_off, bcarry + d.coef_off / 64};
@@ -1230,7 +1220,6 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
       witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rl, base, lp);
     else
       witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rg, base, lp);
-#endif
     if (g.j == sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;

@@ -567,6 +567,20 @@ def slot_streams(depth: int, queues: int, env: Optional[str] = None) -> Tuple[in
     return n_high, slot_dma
 
 
+_slot_stream_sets: dict = {}  # (device index, priority) -> [torch.cuda.Stream]
+
+
+def _slot_stream(dev, priority: int, i: int):
+    """The device's process-wide slot stream i of `priority` (0 normal, -1
+    high), created on first request: DecodePipelines share them (a process's
+    pipelines decode one after another; two used at once serialise on the
+    shared slots, still in order)."""
+    lst = _slot_stream_sets.setdefault((dev.index, priority), [])
+    while len(lst) <= i:
+        lst.append(torch.cuda.Stream(dev, priority=priority))
+    return lst[i]
+
+
 class DecodePipeline:
     """`depth` batches in flight: each slot owns a libldt context (its own HBM
     workspace and pinned staging ring) and a HIP stream. ``decode(batch)``
@@ -625,17 +639,41 @@ class DecodePipeline:
         if slot_dma:
             for c in self.ctxs:
                 c.set_option(_lib.OPT_COPY_MODE, 1)
-        self.streams = [torch.cuda.Stream(self.dec.device, priority=-1 if i < n_high else 0)
-                        for i in range(self.depth)]
-        # adaptive: slots 0 and 1 DMA large batches on slot 2's stream
+        # the slot streams are taken at the first decode (see _streams_now)
+        self._n_high = n_high
+        self._streams = None
         self._copy_mode = [1 if slot_dma else 0] * self.depth
         self._k_large = self._k_small = 0
-        if self.adaptive:
-            for c in self.ctxs[:2]:
-                c.set_copy_stream(self.streams[2])
         self.pending = [deque() for _ in range(self.depth)]  # per slot: (ticket, n), oldest first
         self.last_ticket = None  # (slot, ticket) of the most recent decode
         self.k = 0
+
+    @property
+    def streams(self):
+        """The slots' HIP streams (taken at the first decode)."""
+        return self._streams_now()
+
+    def _streams_now(self):
+        """Slot i's stream is the device's process-wide slot stream i of its
+        priority (_slot_stream), taken at the first decode rather than at
+        construction. The HIP runtime maps a process's streams onto
+        GPU_MAX_HW_QUEUES hardware queues per priority in the order they
+        come to it, and a slot whose queue also carries a stream the process
+        made afterwards lost up to 30% (tools/probes/stream_env.py, DESIGN.md
+        §6): pipelines built before a DDP process group and model (the
+        reference's order, lance_iterable.py:78-95) run their first batch
+        after them, and every pipeline of the process shares the same few
+        slot streams instead of adding new ones that the runtime would place
+        on the queues of the live pipeline's slots."""
+        if self._streams is None:
+            st = [_slot_stream(self.dec.device, -1, i) if i < self._n_high
+                  else _slot_stream(self.dec.device, 0, i - self._n_high) for i in range(self.depth)]
+            self._streams = st
+            # adaptive: slots 0 and 1 DMA large batches on slot 2's stream
+            if self.adaptive:
+                for c in self.ctxs[:2]:
+                    c.set_copy_stream(st[2])
+        return self._streams
 
     def decode(self, batch, normalize=None, image_column: str = "image", label_column: str = "label",
                wait: bool = True):

@@ -1,0 +1,47 @@
+"""The pipeline's rate in a DDP-shaped process.
+
+lance_iterable.py:78-95 builds the dataset (and with it the to_tensor_fn)
+after init_process_group, then wraps the model in DDP, then iterates: the
+decode pipeline's streams exist before RCCL's communicator and DDP's streams
+run their first work, and its first batch comes after them.
+tools/probes/stream_env.py reproduces that order in a fresh process ("ref":
+pipeline built, then a process group with one all_reduce, four side streams
+used once and a comm stream the consumer waits on at every step, then the
+loop), and "prev" (another pipeline of the process used and dropped first).
+Each runs in its own process, because the HIP runtime's stream-to-queue
+mapping is per process; the rates are compared with a clean process's.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+PROBE = os.path.join(REPO, "tools", "probes", "stream_env.py")
+
+
+def _rate(mode, wl, **env):
+    e = dict(os.environ, **env)
+    out = subprocess.run([sys.executable, PROBE, mode, wl, "100"], capture_output=True, text=True, timeout=240,
+                         env=e, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+    return json.loads(line)["img_s"]
+
+
+def test_c2_host_leg_in_reference_process_order():
+    """The c2 host-input leg (make_to_tensor_fn, 256 x 512x512 q90 per call)
+    keeps >= 0.9x its clean-process rate in the reference's DDP order and
+    after an earlier pipeline of the same process."""
+    clean = _rate("clean", "c2")
+    ref = _rate("ref", "c2")
+    prev = _rate("clean", "c2", LDT_PROBE_PREV="1")
+    print(f"c2 host img/s: clean {clean:.0f}, reference order {ref:.0f} ({ref / clean:.3f}), "
+          f"after another pipeline {prev:.0f} ({prev / clean:.3f})")
+    assert ref >= 0.9 * clean, (clean, ref)
+    assert prev >= 0.9 * clean, (clean, prev)
