@@ -254,16 +254,27 @@ int main(int argc, char **argv) {
      * slots in order, sorted by their symbols, and sorted by their blocks */
     int *sym = calloc(nslot, sizeof(int)), *blk = calloc(nslot, sizeof(int)), *ord = calloc(nslot, sizeof(int));
     int *cst = calloc(nslot, sizeof(int)), *psym = calloc(nslot, sizeof(int));
-    long tot_sym = 0;
+    long tot_sym = 0, kz_skip = 0;
     for (int j = 0; j < nslot; j++) {
       St s = cur[j].en; long stop = (long)(j + 1) * S; if (stop > nbitsl) stop = nbitsl;
       int n = 0, nb = 0;
       while (s.p < stop || s.k != 0) { if (s.k == 0) nb++; step(&s); n++; if (s.p >= nbitsl + 64) break; }
       sym[j] = n; blk[j] = nb; tot_sym += n;
+      if (getenv("KZ")) { /* round-6 model: start at the first block start (k = 0) at/after the entry */
+        St z = cur[j].en; int skip = 0;
+        while (z.k != 0) { step(&z); skip++; if (z.p >= nbitsl + 64) break; }
+        kz_skip += skip; sym[j] = n - skip;
+      }
       /* count-mode steps of the slot's phase-1 trajectory (from the guess) */
       St c = {(long)j * S, 0, 0}; int ns = 0, nsym1 = 0;
       while (c.p < stop) { nsym1 += count_step_sim(&c); ns++; }
       cst[j] = ns; psym[j] = nsym1;
+    }
+    {
+      St u = {0, 0, 0}; long uniq = 0;
+      while (u.p < nbitsl && !(u.p >= nbitsl - 8 && u.k == 0)) { step(&u); uniq++; if (u.p >= nbitsl + 64) break; }
+      printf("write symbols %ld (unique decode of the stream %ld), partial blocks re-decoded at range starts %ld\n",
+             tot_sym, uniq, kz_skip);
     }
     for (int mode = 0; mode < 5; mode++) {
       for (int j = 0; j < nslot; j++) ord[j] = j;
