@@ -9,7 +9,7 @@ import sys
 d = sys.argv[1]
 want = sys.argv[2] if len(sys.argv) > 2 else ""
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(f"{d}/p*/**/*counter_collection.csv", recursive=True):
+for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("ldt::", "")
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))

@@ -74,8 +74,10 @@ static int code_len(const Tab *t, long p) {
   for (int l = 1; l <= 16; l++) { int c = w >> (16 - l); if (c <= t->maxcode[l]) return l; }
   return 16;
 }
+static int PEEK_Y = 11; /* LUMA_PEEK env: peek bits of the luma AC count-mode table (the others 11) */
 static int count_step_sim(St *s) {
   if (s->k == 0 || s->k >= 49) { step(s); return 1; }
+  const int W = bcomp[s->b] == 0 ? PEEK_Y : 11;
   const long p0 = s->p; int n = 0, adv = 0;
   for (;;) {
     int c = bcomp[s->b];
@@ -85,7 +87,7 @@ static int count_step_sim(St *s) {
     if (s->k == 0 || adv > 15) break;
     long used = s->p - p0;
     int cl = code_len(&ac[cac[bcomp[s->b]]], s->p);
-    if (used >= 11 || used + cl > 11) break;
+    if (used >= W || used + cl > W) break;
     (void)c;
   }
   return n;
@@ -99,18 +101,20 @@ static int nslot;
 
 /* decode slot j from state e to the first boundary >= its range end; with
  * prev: stop at the first checkpoint equal to prev's (merge). Returns steps. */
+static int COUNT = 0; /* COUNT env: steps are count-mode steps (count_step_sim), not symbols */
+static inline void adv1(St *s) { if (COUNT) count_step_sim(s); else step(s); }
 static int run(int j, St e, const Traj *prev, Traj *out) {
   long stop = (long)(j + 1) * S; if (stop > nbitsl) stop = nbitsl;
   St s = e; int steps = 0; out->en = e; out->ncp = 0;
   long lims[16];
   for (int c = 0; c < NCP; c++) lims[c] = (long)j * S + ((c + 1) * S) / (NCP + 1);
   for (int c = 0; c < NCP; c++) {
-    while (s.p < lims[c] && s.p < stop) { step(&s); steps++; }
+    while (s.p < lims[c] && s.p < stop) { adv1(&s); steps++; }
     if (s.p >= stop) { out->ex = s; return steps; }
     if (prev && prev->ncp > c && eq(prev->cp[c], s)) { out->cp[c] = s; out->ncp = c + 1; out->ex = prev->ex; return steps; }
     out->cp[c] = s; out->ncp = c + 1;
   }
-  while (s.p < stop) { step(&s); steps++; }
+  while (s.p < stop) { adv1(&s); steps++; }
   out->ex = s;
   return steps;
 }
@@ -130,6 +134,8 @@ int main(int argc, char **argv) {
   nbitsl = nbytes * 8;
   S = atol(argv[2]);
   if (getenv("NCP")) NCP = atoi(getenv("NCP"));
+  if (getenv("COUNT")) COUNT = atoi(getenv("COUNT"));
+  if (getenv("LUMA_PEEK")) PEEK_Y = atoi(getenv("LUMA_PEEK"));
   const int spec = atoi(argv[3]);
   const int lanes_cap = argc > 4 ? atoi(argv[4]) : 1024;
   if (S == 0) { S = 256; while ((nbitsl + S - 1) / S > 1024) S += 64; }
