@@ -96,11 +96,6 @@ extern "C" {
                                  CU's LDS leaves; 0: every stream read from
                                  global memory, destuffed by k_destuff_*) --
                                  a study knob                  */
-#define LDT_OPT_BLOCK_DECODE 18 /* 1: the parallel Huffman decoder records each
-                                  block's bit position instead of writing its
-                                  coefficients, and k_block_decode decodes the
-                                  AC symbols, one lane per block;
-                                  0: the decoder's write pass                    */
 #define LDT_OPT_RESIZE_WG_WAVES 15 /* waves (one band each) per k_resize4
                                  workgroup for JPEG sources: 0 default (4),
                                  1, 2 or 4 (tuning knob: 4 keeps 12 waves

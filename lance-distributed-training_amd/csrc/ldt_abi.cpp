@@ -70,9 +70,6 @@ enum HostPhase {
   kHpCount
 };
 
-#ifndef LDT_BLOCK_DECODE_DEFAULT
-#define LDT_BLOCK_DECODE_DEFAULT false
-#endif
 #ifndef LDT_FUSE_DEFAULT
 #define LDT_FUSE_DEFAULT true // experiment builds: -DLDT_FUSE_DEFAULT=false
 #endif
@@ -96,7 +93,6 @@ struct ldt_ctx {
   bool host_timing = false;
   bool debug_counters = false; // LDT_OPT_DEBUG_COUNTERS
   int64_t win_cap = -1;        // LDT_OPT_HUFF_WINDOW: cap on k_huff_image's LDS window (bytes; -1 none)
-  bool block_decode = LDT_BLOCK_DECODE_DEFAULT; // LDT_OPT_BLOCK_DECODE
   CopyPlacement placement; // of the current pool
   static constexpr int kSlots = 2;
   // device cells, one buffer per pinned slot: a copy-stream DMA into one may
@@ -105,7 +101,7 @@ struct ldt_ctx {
   hipEvent_t data_free_ev[kSlots] = {nullptr, nullptr}; // its last reader (Huffman stage) done
   hipEvent_t h2d_ev[kSlots] = {nullptr, nullptr};       // its DMA done (copy stream)
   bool data_used[kSlots] = {false, false};
-  DevBuf d_plan, d_dstuf, d_coef, d_brec, d_bcarry, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt, d_bpos;
+  DevBuf d_plan, d_dstuf, d_coef, d_brec, d_bcarry, d_pcoef, d_dcv, d_planes, d_raw, d_dscnt;
   DevBuf d_perm; // DistributedSampler scratch: 3 int32 arrays of dataset_len
   std::unique_ptr<CopyPool> copier; // host -> pinned copies (created on first use)
   PinBuf h_data[kSlots], h_plan[kSlots];
@@ -921,7 +917,6 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   if ((rc = ensure_dev(c, c->d_dcv, (size_t)coef_blocks * 2 + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_planes, (size_t)plane_total + 64, s))) return rc;
   if ((rc = ensure_dev(c, c->d_dscnt, 16 * (size_t)(n_chunks + 1), s))) return rc;
-  if (c->block_decode && (rc = ensure_dev(c, c->d_bpos, (size_t)coef_blocks * 4 + 64, s))) return rc;
   ht.mark(kHpPlan); // plan blob written, buffers sized
   const uint8_t *dev_cells = data_dev;
   if (!data_dev) {
@@ -980,7 +975,6 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   p.n_chunks = n_chunks;
   p.n_ds_img = n_ds_img;
   p.chunk_img = reinterpret_cast<const int32_t *>(dp + off_chunk);
-  p.block_decode = c->block_decode ? 1 : 0;
   // diagnostic counters only on request: their atomics cost the kernels time
   p.redo = c->debug_counters ? reinterpret_cast<int32_t *>(dp + off_redo) : nullptr;
   p.max_tabs = max_tabs;
@@ -1002,13 +996,11 @@ int decode_core(ldt_ctx *c, const uint8_t *data_host, const uint8_t *data_dev, c
   w.planes = static_cast<uint8_t *>(c->d_planes.p);
   w.status = reinterpret_cast<int32_t *>(dp + off_status);
   w.ds_cnt = static_cast<int4 *>(c->d_dscnt.p);
-  w.bpos = c->block_decode ? static_cast<uint32_t *>(c->d_bpos.p) : nullptr;
 
   HIPCHK(c, launch_destuff(p, w, s));
   prof_mark(c, LDT_STAGE_DESTUFF, s);
   c->coef_dirty = p.n_prog > 0; // until k_idct is enqueued behind k_prog's output
   HIPCHK(c, launch_huff_parallel(p, w, s));
-  HIPCHK(c, launch_block_decode(p, w, s));
   HIPCHK(c, launch_huff_serial(p, w, s));
   HIPCHK(c, launch_prog(p, w, s));
   HIPCHK(c, launch_dc_scan(p, w, s));
@@ -1122,7 +1114,7 @@ void ldt_destroy(ldt_ctx *c) {
   DeviceGuard g(c->device);
   (void)hipDeviceSynchronize();
   DevBuf *dbs[] = {&c->d_data[0], &c->d_data[1], &c->d_plan, &c->d_dstuf, &c->d_coef, &c->d_brec, &c->d_bcarry, &c->d_pcoef, &c->d_dcv,
-                    &c->d_planes, &c->d_raw, &c->d_dscnt, &c->d_bpos};
+                    &c->d_planes, &c->d_raw, &c->d_dscnt};
   for (DevBuf *b : dbs)
     if (b->p) (void)hipFree(b->p);
   for (int k = 0; k < ldt_ctx::kSlots; ++k) {
@@ -1220,9 +1212,6 @@ int ldt_set_option(ldt_ctx *c, int option, int64_t value) {
     return LDT_OK;
   case LDT_OPT_DEBUG_COUNTERS:
     c->debug_counters = value != 0;
-    return LDT_OK;
-  case LDT_OPT_BLOCK_DECODE:
-    c->block_decode = value != 0;
     return LDT_OK;
   case LDT_OPT_RESIZE_IMPL:
     if (value < 0 || value > 2) return set_err(c, LDT_ERR_ARG, "resize impl %lld", (long long)value);

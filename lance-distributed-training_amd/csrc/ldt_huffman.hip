@@ -636,50 +636,6 @@ __device__ __forceinline__ int write_run_lds(RD &R, St &st, const DecW &dec, int
 }
 
 // ---------------------------------------------------------------------------
-// Block-position pass (LDT_OPT_BLOCK_DECODE, round 6): instead of the write
-// pass, the range's count-mode decode from its true entry (the converged
-// trajectory of the rounds, count steps as in phase 1), recording for every
-// block whose DC symbol it decodes the DC difference (record bits 16-31, for
-// the predictor scan) and the bit position after the DC symbol (bpos, in the
-// image's destuffed region). k_block_decode then decodes each block's AC
-// symbols on a lane of its own. Block ownership is the write pass's (a block
-// belongs to the range that decodes its DC symbol), but the range stops at
-// its exit: the last block's AC symbols are the block decoder's. DC symbols
-// use the l1 half of the table word (the value's size); the count-mode half
-// of a DC table holds the same length and advance (ldt_plan.cpp build_huff).
-// Returns the count steps (a diagnostic).
-template <class W, class RS>
-__device__ __forceinline__ int pos_run(Rd<W> &R, St &st, const Dec &dec, int32_t stop, int &cursor, int lim,
-                                       uint32_t *__restrict__ pos_img, const RS &rs, int base) {
-  int bcur = base + cursor;         // the current block (base - 1: none owned yet)
-  const int blast = base + lim - 1; // the last block the range may start
-  bool go = R.pos() < stop && !(st.k == 0 && bcur >= blast);
-  int iters = 0;
-  while (go) {
-    ++iters;
-    const uint32_t pk = R.peek();
-    const bool dcs = st.k == 0;
-    const uint32_t slot = __builtin_amdgcn_ubfe(dcs ? dec.dcseq : dec.acseq, (uint32_t)st.b3, 3u);
-    const uint32_t soff = (slot << 13) + ((dcs || st.k >= 49) ? 0u : 2u);
-    const uint32_t idx4 = (pk >> (32 - kLookBits)) << 2;
-    uint32_t e = *(lds_cu16)(dec.tabs + soff + idx4);
-    if (__builtin_expect(__any((e & 31u) == 0), 0))
-      if ((e & 31u) == 0) e = lookup_long(dec, slot, e, pk, st.b3, !dcs);
-    const uint32_t t = e & 31u;
-    if (dcs) {
-      ++bcur;
-      rs.put(bcur, (uint32_t)ext_value(pk, e) << 16);
-      pos_img[bcur] = (uint32_t)(R.pos() + (int32_t)t);
-    }
-    R.consume((int)t);
-    advance(st, dec, (int)(e >> 9));
-    go = R.pos() < stop && !(st.k == 0 && bcur >= blast);
-  }
-  cursor = bcur - base;
-  return iters;
-}
-
-// ---------------------------------------------------------------------------
 // Serial decoder: one 64-lane workgroup per image, one lane per segment.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_huff_serial(const ImgDesc *__restrict__ descs,
@@ -1060,7 +1016,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
                                              uint32_t *__restrict__ brec,
                                              uint32_t *__restrict__ bcarry,
                                              int32_t *__restrict__ status, int img,
-                                             int32_t *__restrict__ dbg, uint32_t *__restrict__ bpos) {
+                                             int32_t *__restrict__ dbg) {
   const int tid = threadIdx.x;
   const int S = d.sub_bits;
   const int nseg = d.nseg;
@@ -1235,12 +1191,9 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   sh.ex_p[tid] = pre;
   __syncthreads();
   const uint64_t t_scan = dbg ? wall_clock64() : 0;
-  // bpos: the block-position pass (pos_run) replaces the write pass
-  const bool bdec = bpos != nullptr;
   // the count-mode halves are dead: compact the tables, zero the group planes
-  LDS_AS uint8_t *planes = nullptr;
-  DecW decw;
-  if (!bdec) decw = compact_tables(dec, (LDS_AS uint8_t *)dec.tabs, tid, planes);
+  LDS_AS uint8_t *planes;
+  const DecW decw = compact_tables(dec, (LDS_AS uint8_t *)dec.tabs, tid, planes);
 
   // ---- write pass from the true entry ----
   // block records into LDS (the slot state is dead from here) when they fit
@@ -1263,17 +1216,10 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     LDS_AS uint16_t *lp = (LDS_AS uint16_t *)planes + tid;
     const RecLds rl{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry};
     const RecGlob rg{brec + d.coef_off, bcarry + d.coef_off / 64};
-    if (bdec) {
-      uint32_t *pimg = bpos + d.coef_off;
-      if (rec_lds)
-        witers = pos_run(R, st, dec, wstop, cursor, total - bstart, pimg, rl, base);
-      else
-        witers = pos_run(R, st, dec, wstop, cursor, total - bstart, pimg, rg, base);
-    } else if (rec_lds) {
+    if (rec_lds)
       witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rl, base, lp);
-    } else {
+    else
       witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rg, base, lp);
-    }
     if (g.j == sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;
@@ -1323,8 +1269,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     uint32_t *gr = brec + d.coef_off;
     for (int ib = tid; ib < (int)nblk_img; ib += kHuffThreads) gr[ib] = sh.rec[ib];
     uint32_t *gc = bcarry + d.coef_off / 64;
-    if (!bdec) // (the block decoder stores the carries of its runs)
-      for (int c = tid; c < (int)((nblk_img + 63) >> 6); c += kHuffThreads) gc[c] = sh.carry[c];
+    for (int c = tid; c < (int)((nblk_img + 63) >> 6); c += kHuffThreads) gc[c] = sh.carry[c];
   } else {
     dc_scan_image<kHuffThreads>(d, brec + d.coef_off, (LDS_AS int32_t *)&sh);
   }
@@ -1517,9 +1462,9 @@ __device__ __forceinline__ void stage_tables_dma(const HuffTab *__restrict__ hta
 __global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) k_huff_image(
     const ImgDesc *__restrict__ descs, const Segment *__restrict__ segs,
     const HuffTab *__restrict__ htabs, const uint8_t *__restrict__ data,
-    uint8_t *__restrict__ dstuf, const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
+    const uint8_t *__restrict__ dstuf, const int32_t *__restrict__ par_img, int win_bytes, int warm_pct,
     int16_t *__restrict__ coef, uint32_t *__restrict__ brec, uint32_t *__restrict__ bcarry,
-    int32_t *__restrict__ status, int32_t *__restrict__ dbg, uint32_t *__restrict__ bpos) {
+    int32_t *__restrict__ status, int32_t *__restrict__ dbg) {
   __shared__ ImgLds sh;
   const int img = par_img[blockIdx.x];
   if (status[img] != 0) return;
@@ -1550,7 +1495,7 @@ __global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_
   }
   const int64_t need = destuff_region_bytes(d.src_len, d.nseg) + 16;
   const bool in_lds = need <= win_bytes;
-  uint8_t *base = dstuf + d.dst_off; // 16-aligned
+  const uint8_t *base = dstuf + d.dst_off; // 16-aligned
   if (fused) {
     // the planner fuses only images whose stream fits the window
     if (!in_lds) {
@@ -1592,32 +1537,15 @@ __global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_
   }
   __builtin_amdgcn_s_waitcnt(0); // this wave's table DMAs have landed
   __syncthreads();
-  if (bpos && fused) {
-    // the block decoder reads the destuffed stream from memory: the window's
-    // words, byte order restored, into the image's region (its own bytes only:
-    // the next image's region starts right behind it)
-    const int npc = (int)(destuff_region_bytes(d.src_len, d.nseg) / 16);
-    const LDS_AS v4u *wl = (const LDS_AS v4u *)dyn_lds;
-    v4u *gdst = reinterpret_cast<v4u *>(base);
-    for (int i = tid; i < npc; i += kHuffThreads) {
-      const v4u v = wl[i];
-      v4u o;
-      o.x = __builtin_bswap32(v.x);
-      o.y = __builtin_bswap32(v.y);
-      o.z = __builtin_bswap32(v.z);
-      o.w = __builtin_bswap32(v.w);
-      gdst[i] = o;
-    }
-  }
   const uint64_t t_setup = dbg ? wall_clock64() : 0;
   if (dbg && tid == 0) atomicAdd(dbg + 8, (int)(t_setup - t_start));
   const int warm = (d.sub_bits * warm_pct) / 100;
   if (in_lds)
     image_decode(LdsWords{(lds_cu32)dyn_lds}, d, segs, dec, warm, t_setup, sh, coef, brec, bcarry,
-                 status, img, dbg, bpos);
+                 status, img, dbg);
   else
     image_decode(GlobWords{reinterpret_cast<const uint32_t *>(base)}, d, segs, dec, warm, t_setup,
-                 sh, coef, brec, bcarry, status, img, dbg, bpos);
+                 sh, coef, brec, bcarry, status, img, dbg);
 }
 
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s) {
@@ -1629,209 +1557,7 @@ hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t 
   const size_t lds = (size_t)p.win_bytes + huff_tab_lds_image(p.max_tabs);
   hipLaunchKernelGGL(k_huff_image, dim3(p.n_par), dim3(kHuffThreads), lds, s, p.descs, p.segs,
                      p.htabs, w.data, w.dstuf, p.par_img, p.win_bytes, p.warm_pct, w.coef, w.brec, w.bcarry,
-                     w.status, p.redo, p.block_decode ? w.bpos : nullptr);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// k_block_decode (LDT_OPT_BLOCK_DECODE, round 6): the AC coefficients of the
-// parallel decoder's images, one lane per 8x8 block, from the bit position
-// pos_run recorded after the block's DC symbol, in the image's destuffed
-// region (dstuf; k_huff_image copies its LDS window there for fused images).
-// A block's AC symbols are decoded as write_run decodes them (jdhuff.c
-// decode_mcu's AC loop: run/size symbols, ZRL, EOB, k past 63 clamped), the
-// open 16-byte group held in registers. Every block is a run of its own
-// (record bit 8): its nonzero groups go to units 8b, 8b + 1, ... of the
-// image's packed region, which k_idct reads unchanged. The record keeps its
-// DC (bits 16-31, already the absolute value after the predictor scan).
-// Reads past the region's end see zero bits (libjpeg's fill after a marker).
-// ---------------------------------------------------------------------------
-namespace {
-// Big-endian bit reader over global memory words: hi, lo, nxt = words
-// wi-2..wi as Rd, plus the word after nxt loaded one symbol ahead (nl), so a
-// word crossing waits for a load issued a whole symbol (a table lookup)
-// earlier rather than for one issued in the same step.
-struct BlkRd {
-  const uint32_t *w;
-  int nw;
-  uint32_t hi, lo, nxt, nl;
-  int32_t wi, rs;
-  __device__ __forceinline__ uint32_t word(int32_t i) const {
-    const uint32_t v = __builtin_bswap32(w[min(max(i, 0), nw - 1)]);
-    return (i >= 0 && i < nw) ? v : 0u;
-  }
-  __device__ __forceinline__ void seek(int32_t q) {
-    const int32_t i = (q - 1) >> 5;
-    hi = word(i);
-    lo = word(i + 1);
-    nxt = word(i + 2);
-    nl = word(i + 3);
-    wi = i + 2;
-    rs = 32 * (i + 1) - q;
-  }
-  __device__ __forceinline__ uint32_t peek() const { return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)rs); }
-  __device__ __forceinline__ void consume(int t) { // t <= 31
-    const int32_t r2 = rs - t;
-    const bool m = r2 < 0;
-    hi = m ? lo : hi;
-    lo = m ? nxt : lo;
-    nxt = m ? nl : nxt;
-    rs = r2 & 31;
-    wi += m ? 1 : 0;
-    nl = word(wi + 1);
-  }
-};
-} // namespace
-
-// The AC symbols of one block from the reader's position (k = 1 after the DC
-// symbol), the open group in registers; returns the group mask.
-struct WinWords { // a wave's stream window in LDS (big-endian words from word ws)
-  lds_cu32 w;
-  int32_t ws;
-  __device__ __forceinline__ uint32_t operator()(int32_t i) const { return w[i - ws]; }
-};
-template <class RD>
-__device__ __forceinline__ uint32_t block_ac(RD &R, const LDS_AS uint16_t *l1, const LDS_AS uint16_t *l2,
-                                             const HuffTab *__restrict__ htabs, const ImgDesc &d, int bm,
-                                             uint4 *__restrict__ cu) {
-  uint64_t glo = 0, ghi = 0; // the open group: slots 0-3, 4-7
-  int cg = -1;               // its index; < 0: none
-  uint32_t mask = 0;
-  int nu = 0;
-  int k = 1;
-  while (k < 64) {
-    const uint32_t pk = R.peek();
-    uint32_t e = l1[pk >> (32 - kLookBits)];
-    if (__builtin_expect(__any((e & 31u) == 0), 0)) {
-      if ((e & 31u) == 0)
-        e = e == kHuffCanon ? lookup_canon(htabs, &d, bm, true, pk)
-                            : l2[((e >> 5) << kL2Bits) + ((pk >> 16) & ((1u << kL2Bits) - 1))];
-    }
-    const int v = ext_value(pk, e);
-    const int adv = (int)(e >> 9);
-    const int slot = min(k + adv - 1, 63);
-    const int g = slot >> 3;
-    const bool put = (e & (15u << 5)) != 0; // a nonzero value (size != 0)
-    if (put && g != cg) {
-      if (cg >= 0) {
-        cu[nu++] = make_uint4((uint32_t)glo, (uint32_t)(glo >> 32), (uint32_t)ghi, (uint32_t)(ghi >> 32));
-        mask |= 1u << cg;
-      }
-      glo = ghi = 0;
-      cg = g;
-    }
-    const uint64_t x = put ? (uint64_t)((uint32_t)v & 0xFFFFu) << (16 * (slot & 3)) : 0ull;
-    glo |= (slot & 4) ? 0ull : x;
-    ghi |= (slot & 4) ? x : 0ull;
-    R.consume((int)(e & 31u));
-    k += adv;
-  }
-  if (cg >= 0) {
-    cu[nu] = make_uint4((uint32_t)glo, (uint32_t)(glo >> 32), (uint32_t)ghi, (uint32_t)(ghi >> 32));
-    mask |= 1u << cg;
-  }
-  return mask;
-}
-
-constexpr int kBdWinWords = 384; // a wave's stream window (1.5 KB: 192 bits per block)
-
-__global__ void __launch_bounds__(256) k_block_decode(const ImgDesc *__restrict__ descs,
-                                                     const HuffTab *__restrict__ htabs,
-                                                     const uint8_t *__restrict__ dstuf,
-                                                     const int32_t *__restrict__ par_img,
-                                                     const uint32_t *__restrict__ bpos,
-                                                     int16_t *__restrict__ coef, uint32_t *__restrict__ brec,
-                                                     uint32_t *__restrict__ bcarry,
-                                                     const int32_t *__restrict__ status) {
-  // the image's distinct AC tables (l1 entries, l2 parts), and per wave the
-  // stream bits of its 64 blocks, in LDS
-  __shared__ uint16_t s_l1[3][1 << kLookBits];
-  __shared__ uint16_t s_l2[3][kL2Chunks << kL2Bits];
-  __shared__ uint32_t s_win[4][kBdWinWords];
-  const int img = par_img[blockIdx.y];
-  if (status[img] != 0) return;
-  const ImgDesc &d = descs[img];
-  const int nblk = d.mcux * d.mcuy * d.bpm;
-  if ((int)blockIdx.x * 256 >= nblk) return;
-  const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  int tix[3], ns = 0, cslot[3] = {0, 0, 0};
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const int t = d.act[c < d.ncomp ? c : 0];
-    int f = -1;
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      if (q < ns && tix[q] == t) f = q;
-    if (f < 0) {
-      f = ns;
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        if (q == ns) tix[q] = t;
-      ++ns;
-    }
-    cslot[c] = f;
-  }
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    if (q < ns) {
-      const HuffTab *Tq = htabs + tix[q];
-      for (int i = tid; i < (1 << kLookBits); i += 256) s_l1[q][i] = (uint16_t)Tq->lc[i];
-      for (int i = tid; i < (kL2Chunks << kL2Bits); i += 256) s_l2[q][i] = Tq->l2[i];
-    }
-  }
-  // the wave's window: from the word before its first block's AC bits to a
-  // few words past the next wave's first block (its blocks end before that
-  // block's DC symbol); the image's last wave to the region's end
-  const uint32_t *wsrc = reinterpret_cast<const uint32_t *>(dstuf + d.dst_off);
-  const int nw = (int)(destuff_region_bytes(d.src_len, d.nseg) / 4);
-  const int b0 = (int)blockIdx.x * 256 + 64 * wave;
-  const uint32_t *pimg = bpos + d.coef_off;
-  int ws = 0, n = kBdWinWords + 1;
-  if (b0 < nblk) {
-    ws = max(((int)pimg[b0] - 1) >> 5, 0);
-    const int we = b0 + 64 < nblk ? ((int)pimg[b0 + 64] >> 5) + 4 : nw + 4;
-    n = we - ws;
-  }
-  const bool inwin = n <= kBdWinWords;
-  if (inwin)
-    for (int i = lane; i < n; i += 64) {
-      const int gi = ws + i;
-      const uint32_t v = __builtin_bswap32(wsrc[min(gi, nw - 1)]);
-      s_win[wave][i] = gi < nw ? v : 0u;
-    }
-  __syncthreads();
-  const int b = b0 + lane;
-  if (b >= nblk) return;
-  const int bm = b % d.bpm;
-  const int comp = d.bcomp[bm];
-  const int sl = comp == 0 ? cslot[0] : (comp == 1 ? cslot[1] : cslot[2]);
-  const LDS_AS uint16_t *l1 = (const LDS_AS uint16_t *)s_l1[sl];
-  const LDS_AS uint16_t *l2 = (const LDS_AS uint16_t *)s_l2[sl];
-  uint4 *__restrict__ cu = reinterpret_cast<uint4 *>(coef + d.coef_off * 64) + 8 * b;
-  const int32_t q = (int32_t)pimg[b];
-  uint32_t mask;
-  if (inwin) {
-    Rd<WinWords> R;
-    R.src = WinWords{(lds_cu32)s_win[wave], ws};
-    R.seek(q);
-    mask = block_ac(R, l1, l2, htabs, d, bm, cu);
-  } else {
-    BlkRd R;
-    R.w = wsrc;
-    R.nw = nw;
-    R.seek(q);
-    mask = block_ac(R, l1, l2, htabs, d, bm, cu);
-  }
-  uint32_t *rp = brec + d.coef_off + b;
-  *rp = (*rp & 0xFFFF0000u) | 256u | mask;
-  if ((b & 63) == 0) bcarry[(d.coef_off + b) >> 6] = 8u * (uint32_t)b;
-}
-
-hipError_t launch_block_decode(const DevPlan &p, const DevWork &w, hipStream_t s) {
-  if (p.n_par == 0 || !p.block_decode) return hipSuccess;
-  const dim3 grid((unsigned)((p.max_blocks + 255) / 256), (unsigned)p.n_par);
-  hipLaunchKernelGGL(k_block_decode, grid, dim3(256), 0, s, p.descs, p.htabs, w.dstuf, p.par_img, w.bpos, w.coef,
-                     w.brec, w.bcarry, w.status);
+                     w.status, p.redo);
   return hipGetLastError();
 }
 

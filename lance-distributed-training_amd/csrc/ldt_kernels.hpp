@@ -50,7 +50,6 @@ struct DevPlan {
   int n_chunks;
   int n_ds_img;           // baseline images destuffed by k_destuff_* (the others: k_huff_image)
   const int32_t *chunk_img; // chunk -> image
-  int block_decode;         // 1: k_huff_image records block positions, k_block_decode decodes the AC symbols
 };
 
 // Coefficients of baseline images (the Huffman decoders' output), packed:
@@ -97,14 +96,11 @@ struct DevWork {
   uint8_t *planes;      // component planes
   int32_t *status;      // per image
   int4 *ds_cnt;         // per destuff chunk: kept bytes, RSTn markers, end marker seen
-  uint32_t *bpos;       // LDT_OPT_BLOCK_DECODE: per block, the bit position after its DC symbol
 };
 
 hipError_t launch_destuff(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_huff_serial(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_huff_parallel(const DevPlan &p, const DevWork &w, hipStream_t s);
-// LDT_OPT_BLOCK_DECODE: the AC symbols of k_huff_image's images, one lane per block.
-hipError_t launch_block_decode(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_dc_scan(const DevPlan &p, const DevWork &w, hipStream_t s);
 hipError_t launch_idct(const DevPlan &p, const DevWork &w, hipStream_t s);
 // Progressive (SOF2) images: serial per-scan decode into coef/dcv (ldt_prog.hip).

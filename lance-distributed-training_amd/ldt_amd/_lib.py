@@ -62,8 +62,6 @@ OPT_COPY_NT = 14
 OPT_RESIZE_WG_WAVES = 15
 OPT_DEBUG_COUNTERS = 16
 OPT_HUFF_WINDOW = 17
-OPT_BLOCK_DECODE = 18
-BLOCK_DECODE_DEFAULT = 0  # the library's default (ldt_abi.cpp LDT_BLOCK_DECODE_DEFAULT)
 
 STAGES = ("h2d", "destuff", "huffman", "idct", "resize")
 HOST_PHASES = ("slot", "parse", "plan", "copy_join", "launch", "status", "copy_wake", "copy_span")

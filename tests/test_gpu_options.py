@@ -54,29 +54,6 @@ def test_study_options_leave_tensors_unchanged(option_cells, opt, value):
     assert not bad, f"{opt}={value}: images {bad[:10]} differ from the default run"
 
 
-@pytest.mark.parametrize("window", [-1, 0, 16384])
-def test_block_decode_matches_write_pass(option_cells, window):
-    """LDT_OPT_BLOCK_DECODE 1 (the decoder records block positions, k_block_decode
-    decodes each block's AC symbols on its own lane) gives the write pass's
-    tensors bit for bit: stream window in LDS with the fused destuff (-1), every
-    stream in global memory through k_destuff_* (0), and both in one batch (16 KB)."""
-    from ldt_amd import _lib
-
-    ctx = _lib.get_context(0)
-    ctx.set_option(_lib.OPT_HUFF_WINDOW, window)
-    try:
-        ctx.set_option(_lib.OPT_BLOCK_DECODE, 0)
-        base_img, base_lbl = _decode(option_cells)
-        ctx.set_option(_lib.OPT_BLOCK_DECODE, 1)
-        img, lbl = _decode(option_cells)
-    finally:
-        ctx.set_option(_lib.OPT_BLOCK_DECODE, _lib.BLOCK_DECODE_DEFAULT)
-        ctx.set_option(_lib.OPT_HUFF_WINDOW, -1)
-    assert np.array_equal(lbl, base_lbl)
-    bad = [k for k in range(len(option_cells)) if not np.array_equal(img[k], base_img[k])]
-    assert not bad, f"window {window}: images {bad[:10]} differ between block decode and the write pass"
-
-
 def test_debug_counters_only_when_enabled(option_cells):
     """ldt_debug_counters refuses after a batch decoded without the option and
     reports one workgroup per parallel-decoded image with it."""

@@ -10,6 +10,8 @@
  * the start of the next round.
  * Prints rounds and the critical path: the sum over rounds of the longest
  * decode (symbol steps) of the round.
+ * COUNT=1: steps are count-mode steps (LUMA_PEEK: the luma AC peek bits);
+ * BLOCKS=1: the lane-per-block model of round 6's k_block_decode instead.
  * usage: rounds_sim <file.jpg> <S bits (0: auto)> <spec 0/1> [max spec lanes] */
 #include <stdint.h>
 #include <stdio.h>
@@ -132,6 +134,18 @@ int main(int argc, char **argv) {
   bits = malloc(L); nbytes = 0;
   for (long q = scan; q < L - 1; q++) { if (d[q] == 0xFF) { if (d[q + 1] == 0) { bits[nbytes++] = 0xFF; q++; continue; } break; } bits[nbytes++] = d[q]; }
   nbitsl = nbytes * 8;
+  if (getenv("BLOCKS")) {
+    /* lane-per-block decode model (round 6, k_block_decode): AC symbols per
+     * block, and the sum over 64-block waves of the wave's largest count */
+    St s = {0, 0, 0}; int nb = 0; static int cnt[1 << 16];
+    while (s.p < nbitsl - 16 && nb < (1 << 16)) { int n = 0; step(&s); while (s.k != 0) { step(&s); n++; } cnt[nb++] = n; }
+    long tot = 0, summax = 0;
+    for (int b = 0; b < nb; b++) tot += cnt[b];
+    for (int w = 0; w * 64 < nb; w++) { int mx = 0; for (int l = w * 64; l < nb && l < w * 64 + 64; l++) if (cnt[l] > mx) mx = cnt[l]; summax += mx; }
+    printf("blocks %d ac_syms %ld mean %.2f waves %d mean_wave_max %.2f lane_efficiency %.3f\n", nb, tot, (double)tot / nb,
+           (nb + 63) / 64, (double)summax / ((nb + 63) / 64), (double)tot / (64.0 * summax));
+    return 0;
+  }
   S = atol(argv[2]);
   if (getenv("NCP")) NCP = atoi(getenv("NCP"));
   if (getenv("COUNT")) COUNT = atoi(getenv("COUNT"));
