@@ -26,11 +26,20 @@ for wl, fn, n in (("c2", synth.q90_512, 256), ("c1", synth.food101_like, 128), (
         continue
     cells, labels = fn(n, seed=1000)
     rb = ldt_amd.ResidentBatch(cells, labels)
-    rb.decode()
+
+    def dec():
+        try:
+            rb.decode()
+        except _lib.ImageDecodeError:
+            # timing-only study builds (LDT_PROBE_TOLERATE=1) decode nothing valid
+            if os.environ.get("LDT_PROBE_TOLERATE") != "1":
+                raise
+
+    dec()
     # standalone stage times (one batch in flight): 4 batches after a warm one
     ctx.stage_times(reset=True)
     for _ in range(4):
-        rb.decode()
+        dec()
     st = {k: round(v[0] / max(v[1], 1), 4) for k, v in ctx.stage_times(reset=True).items()}
     out = np.zeros(16, np.int32)
     ctx.check(ctx.lib.ldt_debug_counters(ctx.handle, out.ctypes.data, None), "dbg")
