@@ -932,6 +932,7 @@ struct ImgLds {
   int32_t seg_pb[kMaxParSegs];        // segment start: bit position in the window
   int32_t seg_nb[kMaxParSegs];        // segment length in bits
   int32_t scan[kHuffThreads / 64];
+  int32_t scan_need[kHuffThreads / 64]; // the rounds' per-wave needy counts
   int32_t any_changed;
   // fused destuff: per wave, the scan position of the first end-of-scan
   // marker in its lanes' bytes of the current tile (written every tile by
@@ -1064,51 +1065,81 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     __syncthreads(); // states published
     if (dbg && round == 0 && tid == 0) t_ph1 = wall_clock64();
     // A slot whose predecessor's exit equals the entry of its previous
-    // trajectory adopts that trajectory again (exits flip between two values
-    // while an unsynchronised stretch converges); repeated until no slot
-    // changes, so a run of such slots resolves without decoding.
-    // The same reads give this round's needy slots once no slot adopts any
-    // more: the last pass of the loop leaves `need` and the per-wave counts
-    // of the work list behind (one barrier instead of a second pass).
-    bool need;
-    uint64_t bal;
-    for (;;) {
-      bool hit = false;
-      need = false;
-      if (live && g.j > 0) {
-        const int rel = sh.ex_p[tid - 1] - g.j * S;
-        const int pbk = sh.ex_bk[tid - 1];
-        need = rel != (int)sh.en_p[tid] || pbk != (int)sh.en_bk[tid];
-        hit = need && rel == (int)sh.m_en_p[tid] && pbk == (int)sh.m_en_bk[tid];
-      }
-      bal = __ballot(need);
-      const uint64_t hbal = __ballot(hit);
-      if (lane == 0) {
-        sh.scan[wave] = __popcll(bal);
-        if (hbal) atomicAdd(&sh.memo_hits, __popcll(hbal));
-      }
-      if (!__syncthreads_or(hit)) break; // also: every read of the exits is done
-      if (hit) {
-        const uint16_t ep = sh.en_p[tid], ebk = sh.en_bk[tid], nb = sh.nblk[tid], xbk = sh.ex_bk[tid];
-        const int xp = sh.ex_p[tid];
-        sh.en_p[tid] = sh.m_en_p[tid];
-        sh.en_bk[tid] = sh.m_en_bk[tid];
-        sh.ex_p[tid] = (int)sh.m_ex_p[tid] + g.j * S;
-        sh.ex_bk[tid] = sh.m_ex_bk[tid];
-        sh.nblk[tid] = sh.m_nblk[tid];
-        sh.m_en_p[tid] = ep;
-        sh.m_en_bk[tid] = ebk;
-        sh.m_ex_p[tid] = (uint16_t)(xp - g.j * S);
-        sh.m_ex_bk[tid] = xbk;
-        sh.m_nblk[tid] = nb;
-        sh.cp_n[tid] = 0; // the adopted trajectory's checkpoints are not kept
-      }
-      __syncthreads(); // adoptions published
+    // trajectory (its memo) adopts that trajectory again (exits flip between
+    // two values while an unsynchronised stretch converges), so a run of such
+    // slots resolves without decoding. Round 6 resolves the runs in one pass
+    // instead of repeating the test until no slot adopts (~3 passes of two
+    // barriers per round): a slot keeps its trajectory C or adopts its memo M,
+    // and which one is a function of the predecessor's choice: C if the
+    // predecessor's exit equals C's entry, else M if it equals M's entry,
+    // else C (the slot is needy). These maps over {C, M} compose along the
+    // slots, so an inclusive scan (wave shifts, then the waves' totals after
+    // one barrier) gives every slot its choice. A map is 2 bits: bit 0 the
+    // choice after a predecessor on C, bit 1 after one on M (1: M). A
+    // segment's first slot (and an idle lane) is the constant C.
+    uint32_t map = 0u;
+    int pc_rel = 0, pc_bk = 0, pm_rel = 0, pm_bk = 0; // the predecessor's C and M exits, range-relative
+    int ec_p = 0, ec_bk = 0, em_p = 0, em_bk = 0;      // this slot's C and M entries
+    if (live && g.j > 0) {
+      ec_p = sh.en_p[tid];
+      ec_bk = sh.en_bk[tid];
+      em_p = sh.m_en_p[tid];
+      em_bk = sh.m_en_bk[tid]; // 0xFFFF: no memo (no exit has that block phase)
+      pc_rel = sh.ex_p[tid - 1] - g.j * S;
+      pc_bk = sh.ex_bk[tid - 1];
+      pm_rel = (int)sh.m_ex_p[tid - 1] - S;
+      pm_bk = sh.m_ex_bk[tid - 1];
+      // (a predecessor without a memo never chooses M: bit 1 is then unused)
+      const bool c_c = pc_rel == ec_p && pc_bk == ec_bk, c_m = pc_rel == em_p && pc_bk == em_bk;
+      const bool m_c = pm_rel == ec_p && pm_bk == ec_bk, m_m = pm_rel == em_p && pm_bk == em_bk;
+      map = ((!c_c && c_m) ? 1u : 0u) | ((!m_c && m_m) ? 2u : 0u);
     }
+    // f o g on 2-bit maps: image of x under f o g is f's bit at g's image of x
+    auto compose = [](uint32_t f, uint32_t g2) -> uint32_t {
+      return ((f >> (g2 & 1u)) & 1u) | (((f >> ((g2 >> 1) & 1u)) & 1u) << 1);
+    };
+    uint32_t F = map; // the composition over this wave's slots up to this lane
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t pf = (uint32_t)__shfl_up((int)F, off);
+      if (lane >= off) F = compose(F, pf);
+    }
+    if (lane == 63) sh.scan[wave] = (int32_t)F;
+    __syncthreads(); // the waves' maps; also: every read of the slot states is done
+    uint32_t G = 2u;  // identity: the composition over the earlier waves
+    for (int w = 0; w < wave; ++w) G = compose((uint32_t)sh.scan[w], G);
+    const bool on_m = (compose(F, G) & 1u) != 0; // this slot's choice (from C at the image start)
+    bool pred_m = (uint32_t)__shfl_up((int)on_m, 1) != 0;
+    if (lane == 0) pred_m = (G & 1u) != 0;
+    bool need = false;
+    if (live && g.j > 0 && !on_m)
+      need = pred_m ? (pm_rel != ec_p || pm_bk != ec_bk) : (pc_rel != ec_p || pc_bk != ec_bk);
+    const uint64_t bal = __ballot(need);
+    const uint64_t hbal = __ballot(on_m);
+    if (lane == 0) {
+      sh.scan_need[wave] = __popcll(bal);
+      if (hbal) atomicAdd(&sh.memo_hits, __popcll(hbal));
+    }
+    if (on_m) {
+      const uint16_t ep = sh.en_p[tid], ebk = sh.en_bk[tid], nb = sh.nblk[tid], xbk = sh.ex_bk[tid];
+      const int xp = sh.ex_p[tid];
+      sh.en_p[tid] = sh.m_en_p[tid];
+      sh.en_bk[tid] = sh.m_en_bk[tid];
+      sh.ex_p[tid] = (int)sh.m_ex_p[tid] + g.j * S;
+      sh.ex_bk[tid] = sh.m_ex_bk[tid];
+      sh.nblk[tid] = sh.m_nblk[tid];
+      sh.m_en_p[tid] = ep;
+      sh.m_en_bk[tid] = ebk;
+      sh.m_ex_p[tid] = (uint16_t)(xp - g.j * S);
+      sh.m_ex_bk[tid] = xbk;
+      sh.m_nblk[tid] = nb;
+      sh.cp_n[tid] = 0; // the adopted trajectory's checkpoints are not kept
+    }
+    __syncthreads(); // adoptions and the per-wave needy counts published
     int base = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < kHuffThreads / 64; ++w) {
-      const int c = sh.scan[w];
+      const int c = sh.scan_need[w];
       base += w < wave ? c : 0;
       tot += c;
     }
