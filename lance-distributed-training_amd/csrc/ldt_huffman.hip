@@ -932,8 +932,8 @@ struct ImgLds {
   int32_t seg_pb[kMaxParSegs];        // segment start: bit position in the window
   int32_t seg_nb[kMaxParSegs];        // segment length in bits
   int32_t scan[kHuffThreads / 64];
-  int32_t scan_need[kHuffThreads / 64]; // the rounds' per-wave needy counts
-  int32_t any_changed;
+  int32_t nwork;          // the rounds' work list length
+  int32_t any_changed[2]; // a round's exits changed (alternating words)
   // fused destuff: per wave, the scan position of the first end-of-scan
   // marker in its lanes' bytes of the current tile (written every tile by
   // every wave, so no initialisation has to be ordered before other waves'
@@ -1062,8 +1062,18 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
   const int wave = tid >> 6, lane = tid & 63;
   for (int round = 0; round <= kHuffThreads; ++round) {
     ++rounds;
-    __syncthreads(); // states published
+    // phase 1's states published (a later round's are, by the barrier that
+    // ends the round before it)
+    if (round == 0) __syncthreads();
     if (dbg && round == 0 && tid == 0) t_ph1 = wall_clock64();
+    // this round's work-list length and changed flag start at zero (their
+    // last readers, in the rounds before, are past the barrier that ended
+    // the previous round; the flag alternates between two words, so no lane
+    // still reading the previous round's can see this one's reset)
+    if (tid == 0) {
+      sh.nwork = 0;
+      sh.any_changed[round & 1] = 0;
+    }
     // A slot whose predecessor's exit equals the entry of its previous
     // trajectory (its memo) adopts that trajectory again (exits flip between
     // two values while an unsynchronised stretch converges), so a run of such
@@ -1116,9 +1126,26 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
       need = pred_m ? (pm_rel != ec_p || pm_bk != ec_bk) : (pc_rel != ec_p || pc_bk != ec_bk);
     const uint64_t bal = __ballot(need);
     const uint64_t hbal = __ballot(on_m);
+    // the work list: each wave reserves its needy slots' places with one LDS
+    // atomic (any order serves: lane i re-decodes the list's i-th slot)
+    int wbase = 0;
     if (lane == 0) {
-      sh.scan_need[wave] = __popcll(bal);
-      if (hbal) atomicAdd(&sh.memo_hits, __popcll(hbal));
+      if (bal) wbase = atomicAdd(&sh.nwork, (int)__popcll(bal));
+      if (hbal) atomicAdd(&sh.memo_hits, (int)__popcll(hbal));
+    }
+    wbase = __shfl(wbase, 0);
+    if (need) {
+      sh.work[wbase + __popcll(bal & ((1ull << lane) - 1))] = (uint16_t)tid;
+      // the slot's trajectory becomes its memo now, and its entry the
+      // predecessor's exit, so that the lane re-decoding it reads only this
+      // slot's state (no barrier between the re-decodes and the updates)
+      sh.m_en_p[tid] = (uint16_t)ec_p;
+      sh.m_en_bk[tid] = (uint16_t)ec_bk;
+      sh.m_ex_p[tid] = (uint16_t)(sh.ex_p[tid] - g.j * S);
+      sh.m_ex_bk[tid] = sh.ex_bk[tid];
+      sh.m_nblk[tid] = sh.nblk[tid];
+      sh.en_p[tid] = (uint16_t)(pred_m ? pm_rel : pc_rel);
+      sh.en_bk[tid] = (uint16_t)(pred_m ? pm_bk : pc_bk);
     }
     if (on_m) {
       const uint16_t ep = sh.en_p[tid], ebk = sh.en_bk[tid], nb = sh.nblk[tid], xbk = sh.ex_bk[tid];
@@ -1135,40 +1162,29 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
       sh.m_nblk[tid] = nb;
       sh.cp_n[tid] = 0; // the adopted trajectory's checkpoints are not kept
     }
-    __syncthreads(); // adoptions and the per-wave needy counts published
-    int base = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kHuffThreads / 64; ++w) {
-      const int c = sh.scan_need[w];
-      base += w < wave ? c : 0;
-      tot += c;
-    }
-    if (need) sh.work[base + __popcll(bal & ((1ull << lane) - 1))] = (uint16_t)tid;
+    __syncthreads(); // adoptions, the work list and the needy slots' entries published
+    const int tot = sh.nwork;
     if (tid == 0) {
-      sh.any_changed = 0;
       sh.need_lanes += tot;
       sh.need_waves += (tot + 63) >> 6;
     }
-    __syncthreads();
     if (tot == 0) break;
-    int q = -1, np = 0, nbk = 0, nb = 0, ep = 0, ebk = 0;
-    int32_t qstart = 0, qj = 0; // the slot's range start: reader position, segment-relative
-    bool changed = false;
-    Cp cp;
-    cp.n = 0;
     if (tid < tot) {
-      q = sh.work[tid];
+      // re-decode slot q from its new entry; it merges at the first
+      // checkpoint where it meets its previous trajectory (now its memo)
+      const int q = sh.work[tid];
       const SlotGeom h = slot_geom(sh, nseg, S, q);
-      qstart = h.rstart;
-      qj = h.j * S;
-      ep = sh.ex_p[q - 1];
-      ebk = sh.ex_bk[q - 1];
+      const int qj = h.j * S;
+      const int ep = (int)sh.en_p[q] + qj, ebk = sh.en_bk[q];
       const Cp prev = get_cp(sh, q, h.rstart);
-      const int prev_total = sh.nblk[q];
+      const int prev_total = sh.m_nblk[q];
       St st = make_state(ebk);
       Rd<W> R;
       R.src = src;
       R.seek(h.pbias + ep);
+      int np, nbk, nb = 0;
+      Cp cp;
+      cp.n = 0;
       if (count_run<true>(R, h.rstart, h.stop, S, st, dec, nb, cp, prev, prev_total)) {
         np = sh.ex_p[q];
         nbk = sh.ex_bk[q];
@@ -1176,28 +1192,16 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
         np = R.p - h.pbias;
         nbk = st.bk();
       }
-      changed = (np != sh.ex_p[q]) || (nbk != sh.ex_bk[q]);
-    }
-    __syncthreads(); // every read of this round's exits is done
-    if (q >= 0) {
-      // the trajectory being replaced becomes the slot's memo
-      sh.m_en_p[q] = sh.en_p[q];
-      sh.m_en_bk[q] = sh.en_bk[q];
-      sh.m_ex_p[q] = (uint16_t)(sh.ex_p[q] - qj);
-      sh.m_ex_bk[q] = sh.ex_bk[q];
-      sh.m_nblk[q] = sh.nblk[q];
-      sh.en_p[q] = (uint16_t)(ep - qj);
-      sh.en_bk[q] = (uint16_t)ebk;
       sh.nblk[q] = (uint16_t)nb;
-      put_cp(sh, q, cp, qstart);
-      if (changed) {
+      put_cp(sh, q, cp, h.rstart);
+      if (np != sh.ex_p[q] || nbk != sh.ex_bk[q]) {
         sh.ex_p[q] = np;
         sh.ex_bk[q] = (uint16_t)nbk;
-        sh.any_changed = 1;
+        sh.any_changed[round & 1] = 1;
       }
     }
-    __syncthreads();
-    if (!sh.any_changed) break;
+    __syncthreads(); // the round's new states published
+    if (!sh.any_changed[round & 1]) break;
   }
   const uint64_t t_rounds = dbg ? wall_clock64() : 0;
   if (dbg && tid == 0) {
@@ -1519,6 +1523,7 @@ __global__ void __launch_bounds__(kHuffThreads) __attribute__((amdgpu_waves_per_
       sh.seg_first[d.nseg] = l.sub_first + l.sub_count;
     }
     sh.need_lanes = 0;
+    sh.nwork = 0;
     sh.need_waves = 0;
     sh.memo_hits = 0;
     sh.w_syms = 0;
