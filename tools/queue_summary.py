@@ -1,5 +1,5 @@
 """Per (queue, stream): k_prog dispatches and their busy time, from
-rocprofv3 --kernel-trace CSVs (tools/c2p_queue_trace.sh)."""
+rocprofv3 --kernel-trace CSVs (tools/history/c2p_queue_trace.sh)."""
 import collections
 import csv
 import glob
