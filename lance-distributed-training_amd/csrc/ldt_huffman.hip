@@ -477,11 +477,11 @@ __device__ __forceinline__ int write_run(Rd<W> &R, St &st, const Dec &dec, int32
 // issues in nearly every iteration. write_run's register group (two 64-bit
 // halves: a 64-bit shift, selects and ORs to place each value, and selects to
 // clear it) and its unit pairing cost ~20 of its ~100 VALU per iteration.
-// Here the lane's open group lives in 8 LDS planes of u16 (slot q of lane t
-// at planes + q * 2048 + 2 t, so a value lands with one ds_write_b16 at an
-// address of 2 VALU); a flush reads the 8 halves back (LDS loads, no VALU),
-// stores the 16-byte unit at once and writes zeros behind it. The l1 lookup
-// reads the compacted tables (compact_tables).
+// Here the lane's open group lives in 16 bytes of LDS (lane t at planes +
+// 16 t, its dwords rotated by (t >> 3) & 3), so a value lands with one
+// ds_write_b16 at an address of a few VALU; a flush reads the 16 bytes back
+// with one 128-bit LDS load, stores the unit and writes zeros behind it. The
+// l1 lookup reads the compacted tables (compact_tables).
 // ---------------------------------------------------------------------------
 struct DecW {
   lds_cu8 l1;        // compacted l1 entries: slot s at byte s << 12
@@ -554,29 +554,34 @@ __device__ __forceinline__ DecW compact_tables(const Dec &dec, LDS_AS uint8_t *t
   return dw;
 }
 
-// write_run with the open group in the lane's LDS planes (lp = planes + 2 *
-// lane, see above): block ownership, records, carries and the packed units
-// exactly as write_run writes them (units one 16-byte store each).
-// The lane's open group as a 16-byte unit: the 8 plane halves loaded as
-// packed pairs (ds_read_u16_d16 / _d16_hi fill a register's halves without
-// VALU).
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint4 plane_unit(const LDS_AS uint16_t *lp) {
-  uint32_t r[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    s16x2 h;
-    h.x = (short)lp[(2 * d) * kHuffThreads];
-    h.y = (short)lp[(2 * d + 1) * kHuffThreads];
-    r[d] = __builtin_bit_cast(uint32_t, h);
+// The open group from its rotated 16 bytes: stored dword j holds group dword
+// (j - rot) & 3.
+__device__ __forceinline__ uint4 group_unit(const LDS_AS v4u *gp, int rot) {
+  const v4u sv = *gp;
+  uint32_t a = sv.x, b = sv.y, c = sv.z, d = sv.w;
+  if (rot & 2) { // by two dwords
+    const uint32_t t0 = a, t1 = b;
+    a = c; b = d; c = t0; d = t1;
   }
-  return make_uint4(r[0], r[1], r[2], r[3]);
+  if (rot & 1) { // by one
+    const uint32_t t0 = a;
+    a = b; b = c; c = d; d = t0;
+  }
+  return make_uint4(a, b, c, d);
 }
 
+// write_run with the open group in the lane's 16 LDS bytes (see above):
+// block ownership, records, carries and the packed units exactly as write_run
+// writes them (units one 16-byte store each).
 template <class RD, class RS>
 __device__ __forceinline__ int write_run_lds(RD &R, St &st, const DecW &dec, int32_t stop,
                                               int &cursor, int lim, uint4 *__restrict__ coef_img,
-                                              const RS &rs, int base, LDS_AS uint16_t *lp) {
+                                              const RS &rs, int base, LDS_AS v4u *gp) {
+  // the lane's open group as 16 contiguous bytes (one 128-bit read and one
+  // zeroing write per flush instead of 8 + 8 16-bit ones), its dwords rotated
+  // by (lane >> 3) & 3 so that a wave's 16-bit value stores spread over the
+  // banks (lanes 8 apart would otherwise hit the same one)
+  const int rot = ((int)threadIdx.x >> 3) & 3;
   int cg = -1;                       // the open group's index; < 0: none
   uint32_t wu = (uint32_t)base * 8u; // units stored
   uint32_t gmask = 0;                // groups of the current block
@@ -602,14 +607,13 @@ __device__ __forceinline__ int write_run_lds(RD &R, St &st, const DecW &dec, int
     const bool opens = put && g != cg;
     if (cg >= 0 && (first || opens)) {
       // the open group is complete: its unit, then zeros behind it
-      const uint4 u = plane_unit(lp);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) lp[q * kHuffThreads] = 0;
+      const uint4 u = group_unit(gp, rot);
+      *gp = (v4u)(0u);
       coef_img[wu] = u;
       ++wu;
       gmask |= 1u << cg;
     }
-    if (put) lp[(slot & 7) * kHuffThreads] = (uint16_t)v;
+    if (put) ((LDS_AS uint16_t *)gp)[((slot & 7) + 2 * rot) & 7] = (uint16_t)v;
     // a block starts: the previous one's record, then this block's state
     if (first) {
       if (bcur >= base) rs.put(bcur, gmask | (bcur == base ? 256u : 0u) | (dcd << 16));
@@ -625,7 +629,7 @@ __device__ __forceinline__ int write_run_lds(RD &R, St &st, const DecW &dec, int
   }
   if (bcur >= base) {
     if (cg >= 0) {
-      coef_img[wu] = plane_unit(lp);
+      coef_img[wu] = group_unit(gp, rot);
       gmask |= 1u << cg;
       ++wu;
     }
@@ -1248,13 +1252,13 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     R.src = src;
     R.seek(g.pbias + wp);
     uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
-    LDS_AS uint16_t *lp = (LDS_AS uint16_t *)planes + tid;
+    LDS_AS v4u *gp = (LDS_AS v4u *)planes + tid; // the lane's open group
     const RecLds rl{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry};
     const RecGlob rg{brec + d.coef_off, bcarry + d.coef_off / 64};
     if (rec_lds)
-      witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rl, base, lp);
+      witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rl, base, gp);
     else
-      witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rg, base, lp);
+      witers = write_run_lds(R, st, decw, wstop, cursor, total - bstart, cimg, rg, base, gp);
     if (g.j == sub_count - 1 && bstart + cursor + 1 < total) {
       status[img] = 3; // ran out of data
       trunc = true;
