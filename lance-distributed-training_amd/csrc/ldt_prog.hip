@@ -40,6 +40,9 @@ namespace {
 constexpr int kWin = LDT_PROG_WIN;     // scan bytes staged in LDS (per wave)
 constexpr int kChunk = LDT_PROG_CHUNK; // blocks staged per round (one per lane)
 constexpr int kWaves = 4;   // scans of one chain in flight (one wave each)
+#ifndef LDT_PROG_WAVES_EU
+#define LDT_PROG_WAVES_EU 4
+#endif
 
 struct ProgLds {
   union {
@@ -48,6 +51,7 @@ struct ProgLds {
   };
   __attribute__((aligned(16))) int16_t blk[kChunk][64]; // zigzag slots; [0] unused
   int16_t dc[kChunk];
+  int16_t sink[64]; // the other lanes' half of lane 0's coefficient stores
   int64_t bidx[kChunk]; // coefficient-buffer block index of each staged slot
   int win_base, win_lim; // scan offsets of win[0] and one past its last valid byte
   int pos;               // the reader position (for window refills)
@@ -64,11 +68,18 @@ static_assert(sizeof(ProgLds) * 3 >= sizeof(ProgTab) * 4, "DC tables do not fit"
 //   every lane: 4 of the 256 symbol bytes.
 // jdhuff.c jpeg_huff_decode's search (the smallest l with code <= maxcode[l])
 // is the smallest l with peek16 < lim[l]: one compare across the lanes, a
-// ballot and a find-first-set, then two readlanes for the symbol.
+// ballot and a find-first-set. Meanwhile every lane l decodes the peek as if
+// its code were l bits long (shr, voff, the symbol byte fetched from the lane
+// holding it), and one readlane of lane l gives the length and the symbol.
+// The scalar unit, which the serial decode saturates, issues only the
+// find-first-set and the buffer update.
 struct RegTab {
   uint32_t lim;
   int32_t voff;
   uint32_t vals;
+  uint32_t shr;  // lane l in 1..16: 16 - l
+  uint32_t lenb; // lane l: its code length << 8 (lane 17: 16 << 8 | the corrupt symbol)
+  uint32_t symw; // lane l in 1..16: 8 (the symbol byte's width), else 0
 };
 
 // The wave's bit reader: jdhuff.c semantics (MSB first, FF00 -> FF, FF fill
@@ -83,13 +94,32 @@ struct PReader {
   int marker; // 0: none yet; else the marker code reached
 };
 
-// The whole wave runs the decoder with identical values; every value read
-// from LDS or memory passes through readfirstlane, so the compiler keeps the
-// reader state in SGPRs and the control flow on scalar branches (no exec-mask
-// bookkeeping per branch, SALU 64-bit shifts). Stores are made by lane 0.
+// The whole wave runs the decoder with identical values; every value the
+// decoder's state or control flow takes from LDS or memory passes through
+// readfirstlane, so the compiler keeps the reader state in SGPRs and the
+// control flow on scalar branches (no exec-mask bookkeeping per branch, SALU
+// 64-bit shifts). Results that only lanes consume (stored values, correction
+// and new-value masks, the fill's byte assembly) are computed on the VALU
+// (vu / vv below): the kernel is bound by the CUs' scalar issue.
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
+// A lane-held copy of a wave-uniform value: arithmetic on it runs on the
+// VALU, beside the scalar unit that the serial decode saturates. For results
+// that only lanes consume (stored values, masks); the decoder's own state and
+// control flow stay scalar.
+__device__ __forceinline__ uint32_t vu(uint32_t x) {
+  uint32_t r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+// The same for a value already in a VGPR (an LDS read): kept there.
+__device__ __forceinline__ uint32_t vv(uint32_t x) {
+  uint32_t r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
 }
 
 __device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int p) {
@@ -105,21 +135,18 @@ __device__ __forceinline__ int pbyte(const PReader &r, const ProgLds &L, int p) 
 __device__ __forceinline__ void pfill(PReader &r, const ProgLds &L) {
   if (r.marker == 0 && r.pos + 12 <= r.wl) {
     const int o = r.pos - r.wb;
-    const uint32_t a = uni(L.win32[o >> 2]), b = uni(L.win32[(o >> 2) + 1]),
-                   c = uni(L.win32[(o >> 2) + 2]);
+    // on the VALU: the 8 bytes, the 0xFF test, their big-endian placement
+    // below the buffered bits; the wave then reads the 64-bit result back
+    const uint32_t a = vv(L.win32[o >> 2]), b = vv(L.win32[(o >> 2) + 1]), c = vv(L.win32[(o >> 2) + 2]);
     const uint32_t sh = (uint32_t)(o & 3) * 8;
-    // bytes pos..pos+7 in memory order, little-endian words
-    const uint32_t lo = sh ? (a >> sh) | (b << (32 - sh)) : a;
-    const uint32_t hi = sh ? (b >> sh) | (c << (32 - sh)) : b;
-    // any 0xFF byte among the 8?
+    const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(c, b, sh);
     const uint32_t xl = ~lo, xh = ~hi;
     const uint32_t ffm = ((xl - 0x01010101u) & ~xl & 0x80808080u) | ((xh - 0x01010101u) & ~xh & 0x80808080u);
-    if (ffm == 0) {
+    if (__builtin_amdgcn_ballot_w64(ffm != 0) == 0) {
       const int nb = (64 - r.bits) >> 3; // bytes that fit
-      // big-endian bit order: byte i of memory goes to bits 56-8i of the word
+      const int cut = 64 - 8 * nb;        // bits of the 8 bytes that do not
       const uint64_t be = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
-      const uint64_t keep = nb == 8 ? ~0ull : ~(~0ull >> (8 * nb));
-      r.buf |= (be & keep) >> r.bits;
+      r.buf |= uni64(((be >> cut) << cut) >> r.bits);
       r.bits += 8 * nb;
       r.pos += nb;
       return;
@@ -205,23 +232,31 @@ __device__ __forceinline__ RegTab reg_tab(const ProgTab &t, int lane, bool refin
     v = c;
   }
   r.vals = v;
+  r.shr = has ? (uint32_t)(16 - lane) : 0u;
+  r.lenb = has ? (uint32_t)lane << 8 : (lane == 17 ? (16u << 8) | (refine ? 0x20u : 0u) : 0u);
+  r.symw = has ? 8u : 0u;
   return r;
 }
 
 // The symbol (or class) at the front of the buffer, which holds at least 16
 // bits (the caller has filled it); consumes its code. Branch-free: a ballot
-// of peek16 < lim[l] over the lanes, its lowest lane l, two readlanes.
-__device__ __forceinline__ int sym_reg(PReader &r, const RegTab &t, int corrupt_sym) {
+// of peek16 < lim[l] over the lanes, its lowest lane l, one readlane.
+__device__ __forceinline__ int sym_reg(PReader &r, const RegTab &t) {
   const uint32_t w = (uint32_t)(r.buf >> 48);
   const uint64_t hit = __builtin_amdgcn_ballot_w64(w < t.lim);
   const int l = (int)__builtin_ctzll(hit); // 1..17 (lane 17 always matches)
-  const int len = min(l, 16);
-  const int idx = __builtin_amdgcn_readlane(t.voff, l) + (int)(w >> (16 - len));
-  const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)t.vals, (idx >> 2) & 63);
-  const int sym = (int)((word >> ((idx & 3) * 8)) & 0xFF);
-  r.buf <<= len;
-  r.bits -= len;
-  return l > 16 ? corrupt_sym : sym;
+  // Every lane l decodes the peek as if its code were l bits long, on the
+  // VALU (the scalar unit is the kernel's bound): its symbol index, the
+  // symbol byte fetched from the lane that holds it (one ds_bpermute), and
+  // length << 8 | symbol; the wave then reads lane l's.
+  const uint32_t idx = (uint32_t)(t.voff + (int)(w >> t.shr));
+  const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(idx & 0xFCu), (int)t.vals);
+  const uint32_t cand = t.lenb | __builtin_amdgcn_ubfe(word, idx << 3, t.symw);
+  const uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)cand, l);
+  const int clen = (int)(cs >> 8);
+  r.buf <<= clen;
+  r.bits -= clen;
+  return (int)(cs & 0xFFu);
 }
 
 // Lane i's count of the set bits of m below bit i.
@@ -282,23 +317,28 @@ __device__ __forceinline__ void ac_first_chunk(PReader &R, ProgLds &L, const Reg
       continue;
     }
     int16_t *blk = L.blk[slot];
-    for (int k = Ss; k <= Se; ++k) {
+    for (int k = Ss; k <= Se; ++k) { // one loop exit: an EOBr moves k past 63
       if (R.bits < 32) pfill(R, L); // the code (<= 16 bits) and its value bits (<= 15)
-      const int c = sym_reg(R, rt, 0);
+      const int c = sym_reg(R, rt);
       if (((c + 0x10) & 0x10F) == 0) { // EOBr
         const int r = c >> 4;
         eobrun = 1 << r;
         if (r) eobrun += pget(R, L, r);
         --eobrun;
-        break;
+        k = 64;
+        continue;
       }
       const int t = c & 15;
       k += c >> 4;
       if (t) {
-        const int v = pextend((int)(R.buf >> (64 - t)), t) * (1 << Al);
+        // the value on the VALU (t <= 15 bits, all in the buffer's high word);
+        // lane 0 stores it, the other lanes into their sink halves
+        const uint32_t vt = vu((uint32_t)t), vk = vu((uint32_t)min(k, 63));
+        const int v = pextend((int)((uint32_t)(R.buf >> 32) >> (32u - vt)), (int)vt) * (1 << Al);
+        int16_t *dst = w0 ? blk + vk : L.sink + (threadIdx.x & 63);
+        *dst = (int16_t)v;
         R.buf <<= t;
         R.bits -= t;
-        if (w0) blk[min(k, 63)] = (int16_t)v;
       }
     }
   }
@@ -313,10 +353,10 @@ __device__ __forceinline__ void ac_first_chunk(PReader &R, ProgLds &L, const Reg
 // moves the rank q by r + 1, reads its stop P(q) with one readlane, and takes
 // C(q) - C(previous stop) correction bits. The correction bits (which are in
 // position order over the block), the ranks given a new value and the sign
-// bits are accumulated in SGPRs and deposited on the lanes at the block's end
-// as the position masks corr / newm / negm; lane 0 stores them and the lanes
-// apply them after the chunk (corrections first, then the new values, the
-// order jdphuff.c's walk gives).
+// bits collect on the lanes as they are read (lane = rank, VALU) and are
+// gathered to positions at the block's end as the masks corr / newm / negm;
+// lane 0 stores them and the lanes apply them after the chunk (corrections
+// first, then the new values, the order jdphuff.c's walk gives).
 __device__ __forceinline__ uint64_t pget64(PReader &r, const ProgLds &L, int n) {
   if (n <= 32) return (uint32_t)pget(r, L, n);
   const uint64_t hi = (uint32_t)pget(r, L, n - 32);
@@ -367,43 +407,53 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
       const uint32_t dst = in_z ? jz : (uint32_t)nz0 + ((uint32_t)lane - jz);
       const uint32_t val = in_z ? ((uint32_t)lane | (jn << 8)) : ((uint32_t)(Se + 1) | ((uint32_t)ntot << 8));
       const int pc = __builtin_amdgcn_ds_permute((int)(dst * 4), (int)val);
-      int rn = 0; // the rank of the next zero
-      while (true) {
+      int rn = 0;   // the rank of the next zero
+      int last = 0; // the walk's last stop (64 after an EOBr): one loop exit
+      do {
         if (R.bits < 17) pfill(R, L); // the code (<= 16 bits) and the sign bit
-        const int c = sym_reg(R, rt, 0x20);
+        const int c = sym_reg(R, rt);
         if (c & 0x20) { // EOBr
           const int r = c & 15;
           eobrun = 1 << r;
           if (r) eobrun += pget(R, L, r);
-          break;
-        }
-        // a nonzero size takes a sign bit (1: +p1)
-        const int t1 = (c >> 4) & 1;
-        const int sgn = (int)(R.buf >> 63);
-        R.buf <<= t1;
-        R.bits -= t1;
-        const int q = rn + (c & 15); // the stop's zero rank (ZRL: the 16th zero)
-        const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(pc, min(q, 63));
-        const int stop = (int)(e & 0xFF);
-        int nc = (int)(e >> 8) - ccons; // nonzeros passed: one correction bit each
-        if (nc > 32 || nc > R.bits) { // rare: long corrections or a low buffer
-          while (nc > 32) {
-            deposit((uint32_t)pget(R, L, 32), 32);
-            nc -= 32;
+          last = 64;
+        } else {
+          // a nonzero size takes a sign bit (1: +p1), then the corrections
+          const int t1 = (c >> 4) & 1;
+          const uint32_t shi = (uint32_t)(R.buf >> 32); // the sign bit is its bit 31
+          const int q = rn + (c & 15); // the stop's zero rank (ZRL: the 16th zero)
+          const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(pc, min(q, 63));
+          const int stop = (int)(e & 0xFF);
+          int nc = (int)(e >> 8) - ccons; // nonzeros passed: one correction bit each
+          R.buf <<= t1;
+          R.bits -= t1;
+          if ((uint32_t)nc > (uint32_t)min(32, R.bits)) { // rare: long corrections or a low buffer
+            while (nc > 32) {
+              deposit((uint32_t)pget(R, L, 32), 32);
+              nc -= 32;
+            }
+            if (nc > R.bits) pfill(R, L);
           }
-          if (nc > R.bits) pfill(R, L);
+          // lane ccons + j takes correction bit j, the buffer's bit 63 - j
+          // (nc <= 32: all in its high word), on the VALU
+          const uint32_t d = (uint32_t)lane - (uint32_t)ccons;
+          cbv = d < (uint32_t)nc ? ((uint32_t)(R.buf >> 32) >> ((31u - d) & 31u)) & 1u : cbv;
+          ccons += nc;
+          R.buf <<= nc;
+          R.bits -= nc;
+          // the new value's rank, sign and (corrupt data) overflow, on the VALU
+          const uint32_t vq = vu((uint32_t)q), vt1 = vu((uint32_t)t1);
+          const uint32_t vsgn = vu(shi) >> 31;
+          const uint32_t t1i = vq < (uint32_t)nz0 ? vt1 : 0u;
+          rbv = (uint32_t)lane == vq ? (t1i | ((t1i & vsgn) << 1)) : rbv;
+          const bool past = vt1 > t1i;
+          const int vstop = (int)vu((uint32_t)min(stop, 63));
+          ovf = past ? vstop : ovf;
+          ovf_pos = past ? (int)vsgn : ovf_pos;
+          rn = q + 1;
+          last = stop;
         }
-        const uint32_t cv = nc ? (uint32_t)(R.buf >> (64 - nc)) : 0u;
-        deposit(cv, nc);
-        R.buf <<= nc;
-        R.bits -= nc;
-        const int t1i = q < nz0 ? t1 : 0;
-        rbv = lane == q ? (uint32_t)(t1i | ((t1i & sgn) << 1)) : rbv;
-        ovf = (t1 && !t1i) ? min(stop, 63) : ovf;
-        ovf_pos = (t1 && !t1i) ? sgn : ovf_pos;
-        rn = q + 1;
-        if (stop >= Se) break; // the walk's next k is past Se
-      }
+      } while (last < Se); // past Se: the walk's next k is outside the band
     }
     if (eobrun > 0) { // the rest of the band's nonzeros take correction bits
       int nc = ntot - ccons;
@@ -421,6 +471,8 @@ __device__ __forceinline__ void ac_refine_chunk(PReader &R, ProgLds &L, const Re
     const uint64_t corr = __builtin_amdgcn_ballot_w64(in_n && (cb & 1u));
     uint64_t newm = __builtin_amdgcn_ballot_w64(in_z && (rb & 1u));
     uint64_t negm = __builtin_amdgcn_ballot_w64(in_z && (rb & 1u) && !(rb & 2u));
+    ovf = (int)uni((uint32_t)ovf);
+    ovf_pos = (int)uni((uint32_t)ovf_pos);
     if (ovf >= 0) {
       newm |= 1ull << ovf;
       negm = ovf_pos ? (negm & ~(1ull << ovf)) : (negm | (1ull << ovf));
@@ -464,7 +516,7 @@ __device__ __forceinline__ void wave_sync() {
 
 } // namespace
 
-__global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restrict__ descs,
+__global__ void __launch_bounds__(64 * kWaves, LDT_PROG_WAVES_EU) k_prog(const ImgDesc *__restrict__ descs,
                                              const int32_t *__restrict__ prog_img,
                                              const ProgScan *__restrict__ scans,
                                              const ProgTab *__restrict__ ptabs,
@@ -527,7 +579,7 @@ __global__ void __launch_bounds__(64 * kWaves, 4) k_prog(const ImgDesc *__restri
     if (piped && jc % kWaves != wave) continue; // another wave's scan
     const bool wait_prev = piped && jc > 0;
     wave_sync();
-    RegTab rt = {0u, 0, 0u};
+    RegTab rt{};
     if (dcband) {
       for (int k = 0; k < 4; ++k) {
         if (sc.tab[k] < 0) continue;
