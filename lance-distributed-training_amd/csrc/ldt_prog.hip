@@ -40,8 +40,11 @@ namespace {
 constexpr int kWin = LDT_PROG_WIN;     // scan bytes staged in LDS (per wave)
 constexpr int kChunk = LDT_PROG_CHUNK; // blocks staged per round (one per lane)
 constexpr int kWaves = 4;   // scans of one chain in flight (one wave each)
+// 7 waves per SIMD (72 VGPRs): seven chain workgroups per CU, as many as the
+// pipeline's 7 batches in flight can supply. Since the symbol walk left the
+// scalar unit, more resident chains raise the rate (profiles/r6/prog_salu_ab_r6p.txt).
 #ifndef LDT_PROG_WAVES_EU
-#define LDT_PROG_WAVES_EU 4
+#define LDT_PROG_WAVES_EU 7
 #endif
 
 struct ProgLds {
@@ -659,7 +662,7 @@ __global__ void __launch_bounds__(64 * kWaves, LDT_PROG_WAVES_EU) k_prog(const I
         } else {
           int4 *dst = reinterpret_cast<int4 *>(L.blk[lane]);
           uint64_t nz = 0;
-#pragma unroll
+#pragma unroll 4 // (8 would hold 32 VGPRs of loads: spills under the 72-VGPR cap)
           for (int q = 0; q < 8; ++q) {
             const int4 v = reinterpret_cast<const int4 *>(pcoef + d.pcoef_off * 64)[coef_piece((int)blk, q, coef_npad(d))];
             dst[q] = v;
