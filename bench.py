@@ -207,7 +207,7 @@ def main():
                     help="time without the per-stage HIP events (no roofline)")
     ap.add_argument("--depth", type=int, default=None,
                     help="batches in flight (ldt_amd.DecodePipeline: one context + HIP stream each); default 3, "
-                         "7 for progressive workloads (a c2p batch takes ~13 ms on the device)")
+                         "ldt_amd.PROGRESSIVE_DEPTH (5) for progressive workloads (a c2p batch takes ~13 ms on the device)")
     ap.add_argument("--dataset-batches", type=int, default=100,
                     help="batches per rank of one epoch of the dataset legs at N=1 (divided by the world size, at "
                          "least 12, so that the dataset rank 0 writes stays the same size; 0: skip the legs)")
@@ -251,14 +251,16 @@ def main():
                     help="skip the configs[4] (c5) and progressive (c2p) legs of a c2 run")
     args = ap.parse_args()
     progressive = args.workload.endswith("p")
-    # progressive batches spend ~13 ms in k_prog: 7 in flight (4 slots on
-    # high-priority streams, 3 beside the consumer's; profiles/r4/prog_ab_r4.txt)
+    # progressive batches spend ~13 ms in k_prog: ldt_amd.PROGRESSIVE_DEPTH (5)
+    # in flight, 4 slots on high-priority streams and 1 beside the consumer's
+    # (the same rate in a DDP process: DESIGN.md §6)
+    PROG_DEPTH = 5  # == ldt_amd.PROGRESSIVE_DEPTH (not imported before torch here)
     if args.depth is None:
-        args.depth = 7 if progressive else 3
+        args.depth = PROG_DEPTH if progressive else 3
     if args.dataset_depth is None:
         args.dataset_depth = args.depth
     if args.host_depth is None:
-        args.host_depth = 7 if progressive else 0  # 0: make_to_tensor_fn's own choice (depth=None)
+        args.host_depth = PROG_DEPTH if progressive else 0  # 0: make_to_tensor_fn's own choice (depth=None)
 
     import numpy as np
     import torch
@@ -859,9 +861,9 @@ def leg_c5(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
 
 def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     """The c2 images encoded progressive (SOF2), batch
-    256, 7 in flight (DecodePipeline: 4 slots on high-priority streams):
-    `value` with the cells resident (DecodePipeline(depth=7)),
-    `value_host_input` from a host RecordBatch (make_to_tensor_fn(depth=7)); CPU leg: the
+    256, 5 in flight (DecodePipeline: 4 slots on high-priority streams):
+    `value` with the cells resident (DecodePipeline(depth=PROGRESSIVE_DEPTH)),
+    `value_host_input` from a host RecordBatch (make_to_tensor_fn(depth=PROGRESSIVE_DEPTH)); CPU leg: the
     reference map-style DataLoader at this box's CPU share of workers."""
     import numpy as np
     import pyarrow as pa
@@ -875,10 +877,10 @@ def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     rb = ldt_amd.ResidentBatch(cells, labels, device=dev)
     # the resident leg on its own 7-deep pipeline, the host leg on the
     # to_tensor_fn's (both on the device's shared slot streams)
-    pipe = ldt_amd.DecodePipeline(depth=7, device=dev)
+    pipe = ldt_amd.DecodePipeline(depth=ldt_amd.PROGRESSIVE_DEPTH, device=dev)
     for c in pipe.ctxs:
         c.set_option(_lib.OPT_PROFILE, 1)
-    # ~5 ms per batch 7 deep: at least 60 steps, so that fill and drain stay small
+    # ~4 ms per batch 5 deep: at least 60 steps, so that fill and drain stay small
     K = max(args.steps, 60)
     pipe.stage_times(reset=True)
     t = _warm_then_time(lambda: pipe.decode(rb), K, 15, 0.25, barrier, max_over_ranks)
@@ -886,14 +888,14 @@ def leg_c2p(args, dev, world, rank, barrier, max_over_ranks, cpu_ok):
     pipe.check()
     for c in pipe.ctxs:
         c.set_option(_lib.OPT_PROFILE, 0)
-    leg = {"workload": f"c2p: {WORKLOADS['c2p']['desc']}", "per_gpu_batch": B, "pipeline_depth": 7,
+    leg = {"workload": f"c2p: {WORKLOADS['c2p']['desc']}", "per_gpu_batch": B, "pipeline_depth": ldt_amd.PROGRESSIVE_DEPTH,
            "value": round(B * K * world / t, 1), "value_per_gpu": round(B * K / t, 1), "steps": K,
            "compressed_bytes_per_img": round(float(np.mean([len(c) for c in cells])), 1),
            "stages_ms_per_launch": {k: round(v[0] / max(v[1], 1), 4) for k, v in st.items()}}
     del pipe
     host = pa.RecordBatch.from_arrays([pa.array(cells, pa.binary()), pa.array(np.asarray(labels, np.int64))],
                                       names=["image", "label"])
-    fn = ldt_amd.make_to_tensor_fn(depth=7, device=dev)
+    fn = ldt_amd.make_to_tensor_fn(depth=ldt_amd.PROGRESSIVE_DEPTH, device=dev)
     th = _warm_then_time(lambda: fn(host), K, 15, 0.25, barrier, max_over_ranks)
     fn.check()
     leg["value_host_input"] = round(B * K * world / th, 1)

@@ -12,7 +12,7 @@ from ._lib import ImageDecodeError, LdtError, load_library, version  # noqa: F40
 from .dataset import (ArrowDataset, LanceDataset, SafeLanceDataset, dataset,  # noqa: F401
                       get_safe_loader, write_dataset)
 from .sampler import DistributedSampler, FullScanSampler, ShardedBatchSampler, ShardedFragmentSampler  # noqa: F401
-from .transforms import (IMAGENET_MEAN, IMAGENET_STD, DecodePipeline, ResidentBatch, bind_numa, collate_fn,  # noqa: F401
+from .transforms import (IMAGENET_MEAN, IMAGENET_STD, PROGRESSIVE_DEPTH, DecodePipeline, ResidentBatch, bind_numa, collate_fn,  # noqa: F401
                          decode_arrow, decode_tensor_image, make_collate_fn, make_to_tensor_fn,
                          register_host, resize_raw, unregister_host)
 

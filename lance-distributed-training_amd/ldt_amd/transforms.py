@@ -567,6 +567,15 @@ def slot_streams(depth: int, queues: int, env: Optional[str] = None) -> Tuple[in
     return n_high, slot_dma
 
 
+# Batches in flight for progressive (SOF2) datasets: make_to_tensor_fn(depth=
+# PROGRESSIVE_DEPTH). A c2p batch spends ~13 ms in k_prog, so several must be
+# in flight. At 5 (4 slots on high-priority streams, 1 beside the consumer) the
+# rate is the same in a clean process and in a DDP process in the reference's
+# order (62k img/s both); at 7 the clean rate is 5% higher but the DDP order
+# costs 23% (three normal-priority slots share queues with the comm and
+# consumer streams, whose per-step waits then block them). DESIGN.md §6.
+PROGRESSIVE_DEPTH = 5
+
 _slot_stream_sets: dict = {}  # (device index, priority) -> [torch.cuda.Stream]
 
 

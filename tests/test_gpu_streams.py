@@ -27,7 +27,8 @@ PROBE = os.path.join(REPO, "tools", "probes", "stream_env.py")
 
 def _rate(mode, wl, **env):
     e = dict(os.environ, **env)
-    out = subprocess.run([sys.executable, PROBE, mode, wl, "100"], capture_output=True, text=True, timeout=240,
+    steps = "60" if wl == "c2p" else "100"
+    out = subprocess.run([sys.executable, PROBE, mode, wl, steps], capture_output=True, text=True, timeout=240,
                          env=e, cwd=REPO)
     assert out.returncode == 0, out.stderr[-2000:]
     line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
@@ -54,3 +55,15 @@ def test_c2_host_leg_in_reference_process_order():
           f"after another pipeline {prev:.0f} ({prev / clean:.3f})")
     assert ref >= 0.9 * clean, (clean, ref)
     assert prev >= 0.9 * clean, (clean, prev)
+
+
+def test_c2p_host_leg_in_reference_process_order():
+    """The progressive host-input leg (make_to_tensor_fn(depth=
+    PROGRESSIVE_DEPTH), 256 x 512x512 progressive q90 per call) keeps >= 0.9x
+    its clean-process rate in the reference's DDP order. At depth 7 it kept
+    0.77x (three normal-priority slots behind the comm stream's waits); at 5
+    it measured 1.00x."""
+    clean = _rate("clean", "c2p")
+    ref = _rate_at_least(0.9 * clean, "ref", "c2p")
+    print(f"c2p host img/s: clean {clean:.0f}, reference order {ref:.0f} ({ref / clean:.3f})")
+    assert ref >= 0.9 * clean, (clean, ref)

@@ -1,6 +1,8 @@
 """CPU tests of the host-side logic around the kernels: the Arrow dataset
 shim, sampler iteration (with the oracle standing in for the index kernel,
 as the checker), error reporting."""
+import os
+
 import numpy as np
 import pyarrow as pa
 import pytest
@@ -176,6 +178,7 @@ def test_slot_stream_plan():
     assert slot_streams(2, 4) == (0, False)   # c2 host legs: copy stream
     assert slot_streams(3, 4) == (0, True)    # c2 resident: 3 slots + consumer + copy > 4
     assert slot_streams(4, 4) == (4, False)   # all high priority, copy stream beside the consumer
+    assert slot_streams(5, 4) == (4, True)    # progressive default: 4 high + 1 normal
     assert slot_streams(7, 4) == (4, True)    # 4 high + 3 normal: DMA on the slots
     assert slot_streams(8, 4) == (4, True)
     assert slot_streams(6, 8) == (0, False)   # 6 slots + consumer + copy stream fit 8 queues
@@ -272,3 +275,16 @@ def test_register_churn_guard_counts_prefetch_batches(monkeypatch):
              for k in range(40)]
     assert sum(1 for _ in fn.iterate(fresh)) == 40
     assert not fn.registering()
+
+
+def test_progressive_depth_default_agrees_with_bench():
+    """bench.py's progressive legs run at ldt_amd.PROGRESSIVE_DEPTH (it sets
+    its own copy before importing torch)."""
+    import re
+
+    import ldt_amd
+    from conftest import REPO
+
+    src = open(os.path.join(REPO, "bench.py")).read()
+    m = re.search(r"^    PROG_DEPTH = (\d+)", src, re.M)
+    assert m and int(m.group(1)) == ldt_amd.PROGRESSIVE_DEPTH == 5

@@ -4,7 +4,7 @@ One process per run (stream-to-queue binding is per process): creates the
 streams a DDP training process would (lance_iterable.py:80,95: the process
 group and DDP before the loop) BEFORE or AFTER building the to_tensor_fn, then
 times the host-input legs of c2 (make_to_tensor_fn(), adaptive) and c2p
-(make_to_tensor_fn(depth=7)) with a comm-like stream the consumer waits on at
+(make_to_tensor_fn(depth=ldt_amd.PROGRESSIVE_DEPTH)) with a comm-like stream the consumer waits on at
 every step (DDP's gradient all-reduce). usage:
     python tools/probes/stream_env.py clean|before|ref|after [c2|c2p] [steps]
 (ref: the reference's order, lance_iterable.py:78-95: pipeline built, then
@@ -60,7 +60,7 @@ def main():
     comm = side = buf = None
     if mode == "before":
         comm, side, buf = ddp_env(dev)
-    depth = int(os.environ.get("LDT_PROBE_DEPTH", "0")) or (7 if wl == "c2p" else None)
+    depth = int(os.environ.get("LDT_PROBE_DEPTH", "0")) or (ldt_amd.PROGRESSIVE_DEPTH if wl == "c2p" else None)
     if os.environ.get("LDT_PROBE_PREV") == "1":
         # an earlier pipeline of the process (a c2 to_tensor_fn), used, then dropped
         import pyarrow as pa0
