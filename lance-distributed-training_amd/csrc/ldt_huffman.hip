@@ -477,11 +477,10 @@ __device__ __forceinline__ int write_run(Rd<W> &R, St &st, const Dec &dec, int32
 // issues in nearly every iteration. write_run's register group (two 64-bit
 // halves: a 64-bit shift, selects and ORs to place each value, and selects to
 // clear it) and its unit pairing cost ~20 of its ~100 VALU per iteration.
-// Here the lane's open group lives in 16 bytes of LDS (lane t at planes +
-// 16 t, its dwords rotated by (t >> 3) & 3), so a value lands with one
-// ds_write_b16 at an address of a few VALU; a flush reads the 16 bytes back
-// with one 128-bit LDS load, stores the unit and writes zeros behind it. The
-// l1 lookup reads the compacted tables (compact_tables).
+// Here the lane's open group lives in 16 bytes of LDS (group_at), so a value
+// lands with one ds_write_b16 at an address of two VALU; a flush reads the 16
+// bytes back (two 64-bit LDS reads), stores the unit and writes zeros behind
+// it. The l1 lookup reads the compacted tables (compact_tables).
 // ---------------------------------------------------------------------------
 struct DecW {
   lds_cu8 l1;        // compacted l1 entries: slot s at byte s << 12
@@ -508,9 +507,21 @@ __device__ __forceinline__ uint32_t lookup_w(const DecW &dec, const St &st, uint
   return e;
 }
 
+// A lane's open group: 16 bytes at planes + 16 t + 4 (t >> 3). The 4-byte step
+// every 8 lanes spreads a wave's 16-bit value stores over the banks (lanes 8
+// apart would otherwise hit the same one); the group is read and zeroed as
+// two 64-bit halves of 4-byte alignment (ds_read2 / ds_write2). An earlier
+// layout rotated each lane's dwords instead and spent 8 selects per flush
+// undoing the rotation (write phase 83 vs 79 us per c2 image,
+// profiles/r6/write_group_ab_r6wxy.txt).
+typedef uint32_t v4ua __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ LDS_AS v4ua *group_at(LDS_AS uint8_t *planes, int t) {
+  return (LDS_AS v4ua *)(planes + 16 * t + 4 * (t >> 3));
+}
+
 // After the rounds (no lane reads the count-mode halves any more): each
 // table's l1 halves become a 4 KB u16 array at slot << 12, its l2 part moves
-// to (ns << 12) + slot * kL2Bytes, and the group planes at ns *
+// to (ns << 12) + slot * kL2Bytes, and the lanes' groups at ns *
 // kTabCompactBytes (kHuffPlaneBytes, within huff_tab_lds_image) are zeroed.
 // Entries are moved in chunks of 4 per lane in increasing order, each read
 // before a barrier and written after it: entry j moves from byte 4j to 2j, so
@@ -537,11 +548,11 @@ __device__ __forceinline__ DecW compact_tables(const Dec &dec, LDS_AS uint8_t *t
     }
     __syncthreads();
   }
-  // the l2 parts (read above, before any write) below the group planes
+  // the l2 parts (read above, before any write) below the groups
   if (tid < nl2) ((LDS_AS uint32_t *)(tabs + (ns << 12)))[tid] = l2w;
   planes = tabs + ns * kTabCompactBytes;
-  static_assert(kHuffPlaneBytes == 16 * kHuffThreads, "one 16-byte piece per lane");
-  ((LDS_AS v4u *)planes)[tid] = (v4u)(0u);
+  static_assert(kHuffPlaneBytes == 16 * kHuffThreads + 4 * (kHuffThreads / 8), "16 bytes per lane, 4 per 8 lanes");
+  *group_at(planes, tid) = (v4ua)(0u);
   __syncthreads();
   DecW dw;
   dw.l1 = tabs;
@@ -554,34 +565,17 @@ __device__ __forceinline__ DecW compact_tables(const Dec &dec, LDS_AS uint8_t *t
   return dw;
 }
 
-// The open group from its rotated 16 bytes: stored dword j holds group dword
-// (j - rot) & 3.
-__device__ __forceinline__ uint4 group_unit(const LDS_AS v4u *gp, int rot) {
-  const v4u sv = *gp;
-  uint32_t a = sv.x, b = sv.y, c = sv.z, d = sv.w;
-  if (rot & 2) { // by two dwords
-    const uint32_t t0 = a, t1 = b;
-    a = c; b = d; c = t0; d = t1;
-  }
-  if (rot & 1) { // by one
-    const uint32_t t0 = a;
-    a = b; b = c; c = d; d = t0;
-  }
-  return make_uint4(a, b, c, d);
-}
-
-// write_run with the open group in the lane's 16 LDS bytes (see above):
-// block ownership, records, carries and the packed units exactly as write_run
-// writes them (units one 16-byte store each).
+typedef v4ua GroupT;
 template <class RD, class RS>
 __device__ __forceinline__ int write_run_lds(RD &R, St &st, const DecW &dec, int32_t stop,
                                               int &cursor, int lim, uint4 *__restrict__ coef_img,
-                                              const RS &rs, int base, LDS_AS v4u *gp) {
-  // the lane's open group as 16 contiguous bytes (one 128-bit read and one
-  // zeroing write per flush instead of 8 + 8 16-bit ones), its dwords rotated
-  // by (lane >> 3) & 3 so that a wave's 16-bit value stores spread over the
-  // banks (lanes 8 apart would otherwise hit the same one)
-  const int rot = ((int)threadIdx.x >> 3) & 3;
+                                              const RS &rs, int base, LDS_AS GroupT *gp) {
+  // the lane's open group (group_at: 16 contiguous bytes, one read and one
+  // zeroing write per flush instead of 8 + 8 16-bit ones)
+  auto unit = [&]() {
+    const v4ua sv = *gp;
+    return make_uint4(sv.x, sv.y, sv.z, sv.w);
+  };
   int cg = -1;                       // the open group's index; < 0: none
   uint32_t wu = (uint32_t)base * 8u; // units stored
   uint32_t gmask = 0;                // groups of the current block
@@ -607,13 +601,13 @@ __device__ __forceinline__ int write_run_lds(RD &R, St &st, const DecW &dec, int
     const bool opens = put && g != cg;
     if (cg >= 0 && (first || opens)) {
       // the open group is complete: its unit, then zeros behind it
-      const uint4 u = group_unit(gp, rot);
-      *gp = (v4u)(0u);
+      const uint4 u = unit();
+      *gp = (GroupT)(0u);
       coef_img[wu] = u;
       ++wu;
       gmask |= 1u << cg;
     }
-    if (put) ((LDS_AS uint16_t *)gp)[((slot & 7) + 2 * rot) & 7] = (uint16_t)v;
+    if (put) ((LDS_AS uint16_t *)gp)[slot & 7] = (uint16_t)v;
     // a block starts: the previous one's record, then this block's state
     if (first) {
       if (bcur >= base) rs.put(bcur, gmask | (bcur == base ? 256u : 0u) | (dcd << 16));
@@ -629,7 +623,7 @@ __device__ __forceinline__ int write_run_lds(RD &R, St &st, const DecW &dec, int
   }
   if (bcur >= base) {
     if (cg >= 0) {
-      coef_img[wu] = group_unit(gp, rot);
+      coef_img[wu] = unit();
       gmask |= 1u << cg;
       ++wu;
     }
@@ -1252,7 +1246,7 @@ __device__ __forceinline__ void image_decode(W src, const ImgDesc &d,
     R.src = src;
     R.seek(g.pbias + wp);
     uint4 *cimg = reinterpret_cast<uint4 *>(coef + d.coef_off * 64);
-    LDS_AS v4u *gp = (LDS_AS v4u *)planes + tid; // the lane's open group
+    LDS_AS GroupT *gp = group_at(planes, tid); // the lane's open group
     const RecLds rl{(LDS_AS uint32_t *)sh.rec, (LDS_AS uint32_t *)sh.carry};
     const RecGlob rg{brec + d.coef_off, bcarry + d.coef_off / 64};
     if (rec_lds)

@@ -115,9 +115,9 @@ __host__ __device__ inline int huff_tab_lds(int max_tabs) {
 // k_huff_image's table area: the tables as above for phase 1 and the rounds;
 // for the write pass each table's lc part is compacted to its l1 halves (4 KB,
 // then its 512-byte l2 part), and the rest holds the write pass's coefficient
-// group planes (kHuffThreads x 16 B). Sized so that both fit for every image
+// groups (kHuffThreads x 16 B, 4 B of padding per 8 lanes). Sized so that both fit for every image
 // of the batch (ns <= max_tabs distinct tables).
-constexpr int kHuffPlaneBytes = 16 * kHuffThreads;
+constexpr int kHuffPlaneBytes = 16 * kHuffThreads + 4 * (kHuffThreads / 8); // + 4 B per 8 lanes
 constexpr int kTabCompactBytes = (2 << kLookBits) + 2 * (kL2Chunks << kL2Bits);
 __host__ __device__ inline int huff_tab_lds_image(int max_tabs) {
   const int t = max_tabs < 1 ? 1 : max_tabs;
