@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU parity of the current libldt.so, then an A/B of libldt builds
-# (tools/ab_libs.sh). usage: bash tools/r6_ab.sh <tag> <reps> <lib.so>...
+# (tools/ab_libs.sh). usage: bash tools/history/r6_ab.sh <tag> <reps> <lib.so>...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 T=$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Write-pass unit pairing A/B: parity of the paired build, phase times and
 # bench (tools/ab_libs.sh), then a WRITE_SIZE pass per build (per-kernel HBM
-# writes at depth 1). usage: bash tools/r6_ab_pair.sh <tag>
+# writes at depth 1). usage: bash tools/history/r6_ab_pair.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Resize variant: parity of a libldt build on the resize tests, then the A/B
-# (tools/ab_libs.sh). usage: bash tools/r6_ab_resize.sh <tag> <reps> <variant lib> <base lib>
+# (tools/ab_libs.sh). usage: bash tools/history/r6_ab_resize.sh <tag> <reps> <variant lib> <base lib>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 T=$1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Parity of a variant build (LDT_LIBRARY), then an A/B against the shipped
-# libldt.so (tools/ab_libs.sh). usage: bash tools/r6_abv.sh <tag> <variant.so> [reps]
+# libldt.so (tools/ab_libs.sh). usage: bash tools/history/r6_abv.sh <tag> <variant.so> [reps]
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Block-parallel AC decode (LDT_OPT_BLOCK_DECODE): the option tests on the
 # default build, the parity suite on the build that defaults to it, then an
-# A/B against the write pass (tools/ab_libs.sh). usage: bash tools/r6_bdec.sh <tag> [reps]
+# A/B against the write pass (tools/ab_libs.sh). usage: bash tools/history/r6_bdec.sh <tag> [reps]
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Resident c2 bench lines (K=100) of libldt builds, alternated on one box.
-# usage: bash tools/r6_bench_ab.sh <tag> <reps> <lib.so>...
+# usage: bash tools/history/r6_bench_ab.sh <tag> <reps> <lib.so>...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

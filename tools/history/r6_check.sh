@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU call: GPU test suite, the driver-shaped bench line and the
 # stream-environment probe (tools/probes/stream_env.py). Stops at the first
-# failure. usage: bash tools/r6_check.sh <tag> [tests|bench|streams]...
+# failure. usage: bash tools/history/r6_check.sh <tag> [tests|bench|streams]...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 T=$1

@@ -2,7 +2,7 @@
 # Instruction-cache check of the c2 pipeline (3 batches in flight, the kernels
 # co-resident): the SQC counters this ROCm lists, then one --pmc pass of the
 # I-cache counters and one of the wait/issue counters over a short resident
-# bench. usage: bash tools/r6_icache.sh <tag>
+# bench. usage: bash tools/history/r6_icache.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # k_prog variants: progressive parity of each (LDT_LIBRARY), then the c2p
 # resident rate at several depths, interleaved with the shipped libldt.so.
-# usage: bash tools/r6_prog_ab.sh <tag> "<variant.so ...>" "<depths>"
+# usage: bash tools/history/r6_prog_ab.sh <tag> "<variant.so ...>" "<depths>"
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

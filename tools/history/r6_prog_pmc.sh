@@ -2,7 +2,7 @@
 # k_prog instruction mix of one build (LDT_LIBRARY): SALU / VALU / LDS /
 # branch instructions and wave cycles per launch (tools/probes/prog_rate.py
 # at depth 7 under one rocprofv3 --pmc pass).
-# usage: bash tools/r6_prog_pmc.sh <tag> <lib.so>
+# usage: bash tools/history/r6_prog_pmc.sh <tag> <lib.so>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1/pmc_${2%.so}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Fused-destuff byte stores: a timing-only build without them (setup phase
 # only: its output is not a decode), then the skewed-store build's parity and
-# an A/B against the shipped build. usage: bash tools/r6_put.sh <tag>
+# an A/B against the shipped build. usage: bash tools/history/r6_put.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Spread of the resident c2 line on one box: the driver's shape (20 timed
 # steps after 5 warm-up) five times, then 100 timed steps twice.
-# usage: bash tools/r6_spread.sh <tag>
+# usage: bash tools/history/r6_spread.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Stream-environment matrix (tools/probes/stream_env.py): slot priority
-# policies under clean / DDP-before / DDP-after processes. usage: bash tools/r6_streams.sh <tag>
+# policies under clean / DDP-before / DDP-after processes. usage: bash tools/history/r6_streams.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

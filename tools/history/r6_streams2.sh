@@ -1,6 +1,6 @@
 #!/bin/bash
 # Which part of a DDP-like environment created after the pipeline costs the
-# c2 host leg (tools/probes/stream_env.py after c2). usage: bash tools/r6_streams2.sh <tag>
+# c2 host leg (tools/probes/stream_env.py after c2). usage: bash tools/history/r6_streams2.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Own-queue slot streams (LDT_SLOT_OWN_QUEUE=1, ldt_stream_create with a CU
 # mask of every CU) against the shipped streams, clean and DDP-after, c2 and
-# c2p host legs. usage: bash tools/r6_streams3.sh <tag>
+# c2p host legs. usage: bash tools/history/r6_streams3.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

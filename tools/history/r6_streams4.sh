@@ -1,7 +1,7 @@
 #!/bin/bash
 # Slot streams from torch's pool vs the pipeline's own (ldt_stream_create),
 # high priority, c2 adaptive host leg and c2p depth 4: clean / DDP-before /
-# DDP-after / after an earlier pipeline. usage: bash tools/r6_streams4.sh <tag>
+# DDP-after / after an earlier pipeline. usage: bash tools/history/r6_streams4.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

@@ -2,7 +2,7 @@
 # The reference's stream order (probe mode ref) for c2/c2p, normal vs
 # high-priority c2 slots, and the default bench line with and without
 # LDT_SLOT_PRIORITY=1 (every later leg's pipeline draws new pool streams).
-# usage: bash tools/r6_streams5.sh <tag>
+# usage: bash tools/history/r6_streams5.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1

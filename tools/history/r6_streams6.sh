@@ -2,7 +2,7 @@
 # Process-wide slot streams taken at the first decode (DecodePipeline
 # default) vs per-pipeline pool streams taken at construction (round 5,
 # LDT_SLOT_OWN_QUEUE=3), across stream orders; then the default bench line.
-# usage: bash tools/r6_streams6.sh <tag>
+# usage: bash tools/history/r6_streams6.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_$1
